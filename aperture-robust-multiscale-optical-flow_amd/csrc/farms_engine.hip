@@ -1,0 +1,1001 @@
+// farms_engine.hip — MI355X (gfx950) implementation of the FARMS_Flow batch hot
+// path behind the C ABI of include/farms_hip.h.
+//
+// What the reference does (src/vFlow.cpp:223-414), one event at a time:
+//   SAE write -> computeLocalFlow (9-window plane fit, :841-949, :1214-1381)
+//   -> validity gate (:315) -> flow-surface write -> computeTrueFlow (multiscale
+//   pooling, :952-1210) -> record.
+// Every event reads the surfaces as left by all earlier events and itself.
+//
+// How it runs here:
+//   prep    pixel id per event; stable radix sort of event ids by pixel
+//           (hipCUB) -> per-pixel runs in index order; prev/next links.
+//   sweep 1 (local fit)  events in chunks of C1.  The SAE "as of event e" at
+//           pixel q = the last event at q with index <= e: a dense snapshot of
+//           the SAE at chunk start plus, for pixels touched inside the chunk, a
+//           binary search of that pixel's in-chunk run.  One thread per event.
+//   sweep 2 (pooling)    chunks of C2.  Flow state "as of e" is resolved the
+//           same way against a dense flow snapshot.  A per-chunk bitmap marks
+//           cells that can contribute to any event of the chunk (touched in the
+//           chunk, or carrying valid flow younger than the 500 us kill time at
+//           the chunk's time span); one wavefront per valid event walks the
+//           bitmap rows of its 101 x 101 window, lanes = window rows.
+// Local flow depends only on the SAE, pooling only on local flows and times, so
+// these two sweeps reproduce the sequential semantics exactly.
+//
+// Numerics: fp64 throughout, compiled with -ffp-contract=off (no FMA), with the
+// reference's (and Eigen 3.4's) evaluation order for the fit; see DESIGN.md §3.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/farms_hip.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(e_ == hipErrorOutOfMemory ? FARMS_ENOMEM : FARMS_EHIP,         \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)
+
+constexpr double kMaxStamp = 4294967296.0;  // vFlow.h:27
+constexpr double kTsToSec = 1e-6;           // vFlow.h:28
+constexpr double kKillUs = 500.0;           // vFlow.cpp:961
+constexpr int kDefaultFitChunk = 1 << 20;
+constexpr int kDefaultPoolChunk = 1 << 15;
+constexpr int kMaxScales = 16;
+
+// Local-flow state of one event, and the flow surface cell (x-major).  L = 0 for
+// an invalid event (vFlow.cpp:398-402); Lc/Ls = L*cos(theta), L*sin(theta), the
+// per-visit products of vFlow.cpp:1007-1008 evaluated once per event.
+struct __attribute__((aligned(32))) FlowCell {
+    double L, Lc, Ls;
+    uint32_t t;
+    uint32_t pad;
+};
+
+struct Ctx {
+    int W, H, n;
+    int64_t WH;
+    int fr, min_inl, J, M;
+    const int32_t *x, *y, *p;
+    const uint32_t *t;
+    const uint32_t *pix;   // x*H + y per event
+    const uint32_t *skey;  // pixel ids, sorted
+    const int32_t *P;      // event ids sorted by (pixel, id)
+    const int32_t *pos;    // inverse of P
+    const int32_t *prev, *next;
+    int64_t *touch;        // (chunk seq << 32) | position of the first in-chunk event
+    int32_t *touch_last;   // position of the last in-chunk event
+    int64_t *sae;          // SAE snapshot: -1 never visited, else t
+    FlowCell *fsnap;       // flow snapshot
+    int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
+    FlowCell *evf;         // per-event local flow
+    uint8_t *valid;
+    uint64_t *bitmap;
+    const uint32_t *ctmin, *ctmax;  // per pooling chunk
+    // outputs
+    double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
+    int32_t *scale;
+    int32_t *ox, *oy, *ot, *op;
+    unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells
+};
+
+// ---------------------------------------------------------------------------
+// as-of lookup: position in P of the last event at pixel q with id <= e inside
+// the current chunk, or -1 when the snapshot (state before the chunk) applies.
+__device__ __forceinline__ int asof_pos(const Ctx &c, uint32_t q, int e, uint32_t seq) {
+    const int64_t tw = c.touch[q];
+    if ((uint32_t)((uint64_t)tw >> 32) != seq) return -1;
+    const int k = (int)(uint32_t)tw;
+    if (c.P[k] > e) return -1;
+    int hi = c.touch_last[q];
+    if (hi <= k) return k;
+    if (c.P[hi] <= e) return hi;
+    int lo = k;  // P[lo] <= e < P[hi], P ascending over the run
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (c.P[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// SAE stamp of pixel q as of event e: -1 never visited, else t.
+__device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
+    const int k = asof_pos(c, q, e, seq);
+    if (k >= 0) return (int64_t)c.t[c.P[k]];
+    return c.sae[q];
+}
+
+__device__ __forceinline__ FlowCell flow_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
+    const int k = asof_pos(c, q, e, seq);
+    if (k >= 0) return c.evf[c.P[k]];
+    return c.fsnap[q];
+}
+
+// ---------------------------------------------------------------------------
+// prep
+
+__global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, int *err) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c.n) return;
+    const int x = c.x[e], y = c.y[e];
+    if (x < 0 || x >= c.W || y < 0 || y >= c.H) {
+        atomicOr(err, 1);
+        pix[e] = 0;
+    } else {
+        pix[e] = (uint32_t)x * (uint32_t)c.H + (uint32_t)y;
+    }
+    iota[e] = e;
+}
+
+__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    const int e = c.P[k];
+    const uint32_t q = c.skey[k];
+    pos[e] = k;
+    prev[e] = (k > 0 && c.skey[k - 1] == q) ? c.P[k - 1] : -1;
+    next[e] = (k + 1 < c.n && c.skey[k + 1] == q) ? c.P[k + 1] : INT_MAX;
+}
+
+// per pooling chunk: min / max of t (general streams need not be time-sorted)
+__global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tmin, uint32_t *tmax) {
+    const int ch = blockIdx.x;
+    const int64_t b = (int64_t)ch * chunk;
+    const int64_t e1 = b + chunk < n ? b + chunk : n;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (int64_t e = b + threadIdx.x; e < e1; e += blockDim.x) {
+        const uint32_t v = t[e];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    __shared__ uint32_t slo[256], shi[256];
+    slo[threadIdx.x] = lo;
+    shi[threadIdx.x] = hi;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            slo[threadIdx.x] = min(slo[threadIdx.x], slo[threadIdx.x + s]);
+            shi[threadIdx.x] = max(shi[threadIdx.x], shi[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tmin[ch] = slo[0];
+        tmax[ch] = shi[0];
+    }
+}
+
+// first / last in-chunk event of every pixel touched by chunk [c0, c1)
+__global__ void k_touch(Ctx c, int c0, int c1, uint32_t seq) {
+    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c1) return;
+    const uint32_t q = c.pix[e];
+    if (c.prev[e] < c0) c.touch[q] = (int64_t)(((uint64_t)seq << 32) | (uint32_t)c.pos[e]);
+    if (c.next[e] >= c1) c.touch_last[q] = c.pos[e];
+}
+
+__global__ void k_sae_update(Ctx c, int c0, int c1) {
+    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c1) return;
+    if (c.next[e] >= c1) c.sae[c.pix[e]] = (int64_t)c.t[e];
+}
+
+__global__ void k_flow_update(Ctx c, int c0, int c1) {
+    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c1) return;
+    if (c.next[e] >= c1) {
+        const uint32_t q = c.pix[e];
+        const FlowCell f = c.evf[e];
+        c.fsnap[q] = f;
+        c.ftime[q] = f.L > 0 ? (int64_t)f.t : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Eigen 3.4 PartialPivLU<MatrixXd>::determinant() of the 3x3 normal matrix
+// (vFlow.cpp:1316); a is column-major (AtA.data()).  See oracle for the rules.
+__device__ __forceinline__ double det3_partialpivlu(const double a[9]) {
+    double m00 = a[0], m01 = a[3], m02 = a[6];
+    double m10 = a[1], m11 = a[4], m12 = a[7];
+    double m20 = a[2], m21 = a[5], m22 = a[8];
+    int tr = 0;
+    // k = 0
+    {
+        int piv = 0;
+        double big = fabs(m00);
+        if (fabs(m10) > big) { big = fabs(m10); piv = 1; }
+        if (fabs(m20) > big) { big = fabs(m20); piv = 2; }
+        if (big != 0.0) {
+            if (piv == 1) { double t0 = m00, t1 = m01, t2 = m02; m00 = m10; m01 = m11; m02 = m12; m10 = t0; m11 = t1; m12 = t2; ++tr; }
+            else if (piv == 2) { double t0 = m00, t1 = m01, t2 = m02; m00 = m20; m01 = m21; m02 = m22; m20 = t0; m21 = t1; m22 = t2; ++tr; }
+            m10 = m10 / m00;
+            m20 = m20 / m00;
+        }
+        m11 = m11 - m10 * m01; m12 = m12 - m10 * m02;
+        m21 = m21 - m20 * m01; m22 = m22 - m20 * m02;
+    }
+    // k = 1
+    {
+        double big = fabs(m11);
+        int piv = 1;
+        if (fabs(m21) > big) { big = fabs(m21); piv = 2; }
+        if (big != 0.0) {
+            if (piv == 2) { double t0 = m10, t1 = m11, t2 = m12; m10 = m20; m11 = m21; m12 = m22; m20 = t0; m21 = t1; m22 = t2; ++tr; }
+            m21 = m21 / m11;
+        }
+        m22 = m22 - m21 * m12;
+    }
+    const double prod = (m00 * m11) * m22;
+    return (tr & 1) ? -prod : prod;
+}
+
+// ---------------------------------------------------------------------------
+// Local plane fit, one thread per event.  FR > 0: fRad known at compile time
+// (stamps of the chosen window kept in registers); FR == 0: any fRad.
+template <int FR>
+__global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq) {
+    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c1) return;
+    const int fr = FR > 0 ? FR : c.fr;
+    const int side = 2 * fr + 1;
+    const int np = side * side;
+    const int W = c.W, H = c.H;
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t te = c.t[e];
+
+    // ---- window scores (vFlow.cpp:870-912): sum over the window of
+    // (t_e - t_k) + 2^32 [t_k > t_e], exact as int64; ties: first strict min.
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * fr, cj = ey + (w % 3 - 1) * fr;
+        wok[w] = ci - fr >= 0 && ci + fr <= W - 1 && cj - fr >= 0 && cj + fr <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    double vx = 0.0, vy = 0.0;
+    if (any) {
+#pragma unroll
+        for (int du = -2 * FR; du <= 2 * FR; ++du) {
+            if (FR == 0) break;
+            const int u = ex + du;
+            if (u < 0 || u >= W) continue;
+#pragma unroll
+            for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
+                const int v = ey + dv;
+                if (v < 0 || v >= H) continue;
+                int mask = 0;
+#pragma unroll
+                for (int w = 0; w < 9; ++w) {
+                    const int ou = (w / 3 - 1) * FR, ov = (w % 3 - 1) * FR;
+                    if (du - ou <= FR && ou - du <= FR && dv - ov <= FR && ov - dv <= FR && wok[w]) mask |= 1 << w;
+                }
+                if (!mask) continue;
+                const int64_t st = sae_asof(c, (uint32_t)u * (uint32_t)H + (uint32_t)v, e, seq);
+                const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+                const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+                for (int w = 0; w < 9; ++w)
+                    if (mask & (1 << w)) score[w] += d;
+            }
+        }
+        if (FR == 0) {
+            for (int du = -2 * fr; du <= 2 * fr; ++du) {
+                const int u = ex + du;
+                if (u < 0 || u >= W) continue;
+                for (int dv = -2 * fr; dv <= 2 * fr; ++dv) {
+                    const int v = ey + dv;
+                    if (v < 0 || v >= H) continue;
+                    int mask = 0;
+#pragma unroll
+                    for (int w = 0; w < 9; ++w) {
+                        const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
+                        if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
+                    }
+                    if (!mask) continue;
+                    const int64_t st = sae_asof(c, (uint32_t)u * (uint32_t)H + (uint32_t)v, e, seq);
+                    const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+                    const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+                    for (int w = 0; w < 9; ++w)
+                        if (mask & (1 << w)) score[w] += d;
+                }
+            }
+        }
+        // bestscore starts at MAXSTAMP + 1; sums compare exactly
+        const int64_t nn = np;
+        int64_t best = nn * ((int64_t(1) << 32) + 1);
+        int bw = -1;
+#pragma unroll
+        for (int w = 0; w < 9; ++w)
+            if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+        if (bw >= 0 && !(best > nn * (int64_t(1) << 32))) {
+            // ---- gather the winning window, cx-major (vFlow.cpp:923-930)
+            const int bi = ex + (bw / 3 - 1) * fr, bj = ey + (bw % 3 - 1) * fr;
+            constexpr int NPC = FR > 0 ? (2 * FR + 1) * (2 * FR + 1) : 1;
+            uint32_t tks[NPC];
+            uint64_t vis = 0;
+            int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
+            auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+                const int cx = bi + k / side - fr, cy = bj + k % side - fr;
+                if (FR > 0) {
+                    const bool vk = (vis >> k) & 1;
+                    X = vk ? cx : 0; Y = vk ? cy : 0; T = tks[k < NPC ? k : 0];
+                } else {
+                    const int64_t st = sae_asof(c, (uint32_t)cx * (uint32_t)H + (uint32_t)cy, e, seq);
+                    X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
+                }
+            };
+            if (FR > 0) {
+#pragma unroll
+                for (int k = 0; k < NPC; ++k) {
+                    const int cx = bi + k / (2 * FR + 1) - FR, cy = bj + k % (2 * FR + 1) - FR;
+                    const int64_t st = sae_asof(c, (uint32_t)cx * (uint32_t)H + (uint32_t)cy, e, seq);
+                    tks[k] = st >= 0 ? (uint32_t)st : 0u;
+                    if (st >= 0) vis |= uint64_t(1) << k;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < np; ++k) {
+                int64_t X, Y; uint32_t T;
+                cell(k, X, Y, T);
+                sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+            }
+            // AtA, column-major (vFlow.cpp:1311)
+            const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                                 (double)sy,  (double)sx,  (double)sy, (double)np};
+            double DET = det3_partialpivlu(a);
+            int inliers = 0;
+            double dtdx = 0.0, dtdy = 0.0;
+            if (!(DET < 1)) {
+                DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+                const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+                const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+                const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+                const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+                const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+                const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+                const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+                const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+                const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+                // temp = (A2*At)*Y in Eigen's order
+                const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+                const double cz = (double)te * kTsToSec;
+                double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll
+                for (int k = 0; k < np; ++k) {
+                    int64_t Xi, Yi; uint32_t T;
+                    cell(k, Xi, Yi, T);
+                    const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+                    const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+                    double m0, m1, m2;
+                    if (gemm) {
+                        m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+                        m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+                        m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+                    } else {
+                        m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+                        m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+                        m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+                    }
+                    if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+                    else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+                }
+                if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+                // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+                const double dtdp = sqrt(r0 * r0 + r1 * r1);
+                const double ccx = (double)ex, ccy = (double)ey;
+#pragma unroll
+                for (int k = 0; k < np; ++k) {
+                    int64_t Xi, Yi; uint32_t T;
+                    cell(k, Xi, Yi, T);
+                    const double Tk = (double)T;
+                    const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+                    const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+                    const double actualdt = yt - cz;
+                    if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+                }
+                const double speed = 1.0 / dtdp;
+                const double angle = atan2(r0, r1);
+                dtdx = speed * cos(angle);
+                dtdy = speed * sin(angle);
+            }
+            if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
+        }
+    }
+    // ---- validity gate and flow-surface value (vFlow.cpp:315-357, 384-403)
+    const bool ok = !isnan(fabs(vx)) && !isnan(fabs(vy)) && vx != 0 && vy != 0;
+    FlowCell f;
+    f.t = te;
+    f.pad = 0;
+    double L = 0.0, th = 0.0;
+    if (ok) {
+        L = sqrt(vx * vx + vy * vy);
+        th = atan2(vy, vx);
+        f.L = L;
+        f.Lc = L * cos(th);
+        f.Ls = L * sin(th);
+    } else {
+        f.L = 0.0; f.Lc = 0.0; f.Ls = 0.0;
+    }
+    c.evf[e] = f;
+    c.valid[e] = ok ? 1 : 0;
+    c.vx[e] = vx;
+    c.vy[e] = vy;
+    c.r_local[e] = L;
+    c.th_local[e] = th;
+    if (!ok) { c.r_true[e] = 0.0; c.th_true[e] = 0.0; c.scale[e] = 0; }
+    if (c.ox) { c.ox[e] = ex; c.oy[e] = ey; c.ot[e] = (int32_t)te; c.op[e] = c.p[e]; }
+}
+
+// ---------------------------------------------------------------------------
+// Candidate-cell bitmap for pooling chunk [c0, c1): bit q set if q is touched in
+// the chunk, or its snapshot flow is valid and within the kill time of some
+// event of the chunk.  One wave ballot per 64 cells.
+__global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool act = false;
+    if (q < c.WH) {
+        const int64_t tw = c.touch[q];
+        act = (uint32_t)((uint64_t)tw >> 32) == seq;
+        if (!act) {
+            const int64_t ft = c.ftime[q];
+            const int64_t lo = (int64_t)c.ctmin[chunk_idx] - (int64_t)kKillUs;
+            const int64_t hi = (int64_t)c.ctmax[chunk_idx] + (int64_t)kKillUs;
+            act = ft >= 0 && ft > lo && ft < hi;
+        }
+    }
+    const uint64_t b = __ballot(act);
+    if ((threadIdx.x & 63) == 0) c.bitmap[q >> 6] = b;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Multiscale pooling (computeTrueFlow, vFlow.cpp:952-1210): one wavefront per
+// valid event; lane l walks window rows i = i_lo + l, i_lo + l + 64.  Window rows
+// span x-major linear indices [i*H + j_lo, i*H + j_hi] with j clipped to W-1 as
+// the reference does (vFlow.cpp:1000/1113), so for W > H a row runs into the
+// next column (aliasing kept); indices >= W*H do not contribute.
+template <int K>
+__global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t seq) {
+    const int lane = threadIdx.x & 63;
+    const int e = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (e >= c1) return;
+    if (!c.valid[e]) return;
+    const int ex = c.x[e], ey = c.y[e];
+    const double te = (double)c.t[e];
+    const int W = c.W, H = c.H, M = c.M, J = c.J;
+    const int64_t WH = c.WH;
+    const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
+    const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
+    double sL[K], sX[K], sY[K];
+    int cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) { sL[k] = 0.0; sX[k] = 0.0; sY[k] = 0.0; cnt[k] = 0; }
+    for (int i = i_lo + lane; i <= i_hi; i += 64) {
+        const int64_t base = (int64_t)i * H;
+        const int64_t l0 = base + j_lo;
+        int64_t l1 = base + j_hi;
+        if (l1 > WH - 1) l1 = WH - 1;
+        if (l0 > l1) continue;
+        for (int64_t w = l0 >> 6; w <= (l1 >> 6); ++w) {
+            uint64_t bits = c.bitmap[w];
+            const int64_t wb = w << 6;
+            if (wb < l0) bits &= ~0ull << (l0 - wb);
+            if (wb + 63 > l1) bits &= ~0ull >> (63 - (l1 - wb));
+            while (bits) {
+                const int b = __builtin_ctzll(bits);
+                bits &= bits - 1;
+                const int64_t lin = wb + b;
+                const FlowCell f = flow_asof(c, (uint32_t)lin, e, seq);
+                if (f.L > 0 && fabs(te - (double)f.t) < kKillUs) {  // vFlow.cpp:1002/1115
+                    const int j = (int)(lin - base);
+                    const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
+                    const int d = di > dj ? di : dj;
+                    const int k0 = (d + J - 1) / J;  // smallest scale containing the cell
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (k >= k0) { sL[k] += f.L; sX[k] += f.Lc; sY[k] += f.Ls; cnt[k] += 1; }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        sL[k] = wave_sum(sL[k]);
+        sX[k] = wave_sum(sX[k]);
+        sY[k] = wave_sum(sY[k]);
+        cnt[k] = wave_sum_i(cnt[k]);
+    }
+    if (lane == 0) {
+        // per-scale means, first strict max of mean length (vFlow.cpp:1023-1075)
+        double maxv = 0.0, gx = 0.0, gy = 0.0;
+        int mi = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double mean = cnt[k] > 0 ? sL[k] / (double)cnt[k] : 0.0;
+            if (mean > maxv) { maxv = mean; mi = k; }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k == mi) {
+                gx = cnt[k] > 0 ? sX[k] / (double)cnt[k] : 0.0;
+                gy = cnt[k] > 0 ? sY[k] / (double)cnt[k] : 0.0;
+            }
+        int sc = mi * J;
+        if (!(maxv > 0)) {  // vFlow.cpp:1085-1094
+            const FlowCell self = c.evf[e];
+            gx = self.Lc; gy = self.Ls; sc = 0;
+        }
+        c.r_true[e] = sqrt(gy * gy + gx * gx);  // vFlow.cpp:365-366
+        c.th_true[e] = atan2(gy, gx);
+        c.scale[e] = sc;
+    }
+}
+
+// Algorithmic-work counters for the roofline: U_loc per event,
+// U_pool per valid event, valid count.  Grid-stride, one atomic per block.
+__global__ void k_stats(Ctx c) {
+    unsigned long long nv = 0, usae = 0, upool = 0;
+    const int fr = c.fr;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < c.n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int x = c.x[e], y = c.y[e];
+        const int u0 = max(0, x - 2 * fr), u1 = min(c.W - 1, x + 2 * fr);
+        const int v0 = max(0, y - 2 * fr), v1 = min(c.H - 1, y + 2 * fr);
+        usae += (unsigned long long)(u1 - u0 + 1) * (unsigned long long)(v1 - v0 + 1);
+        if (c.valid[e]) {
+            ++nv;
+            const int i_lo = max(0, x - c.M), i_hi = min(c.W - 1, x + c.M);
+            const int j_lo = max(0, y - c.M), j_hi = min(c.W - 1, y + c.M);
+            for (int i = i_lo; i <= i_hi; ++i) {
+                const int64_t l0 = (int64_t)i * c.H + j_lo;
+                int64_t l1 = (int64_t)i * c.H + j_hi;
+                if (l1 > c.WH - 1) l1 = c.WH - 1;
+                if (l1 >= l0) upool += (unsigned long long)(l1 - l0 + 1);
+            }
+        }
+    }
+    __shared__ unsigned long long s[3][256];
+    s[0][threadIdx.x] = nv; s[1][threadIdx.x] = usae; s[2][threadIdx.x] = upool;
+    __syncthreads();
+    for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st)
+            for (int r = 0; r < 3; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int r = 0; r < 3; ++r) atomicAdd(&c.counters[r], s[r][0]);
+}
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+// ===========================================================================
+// handle
+
+struct farms_handle {
+    farms_params prm;
+    int W = 0, H = 0, fr = 0, J = 0, M = 0, K = 0;
+    int64_t WH = 0;
+    int fit_chunk = kDefaultFitChunk, pool_chunk = kDefaultPoolChunk;
+    hipStream_t stream = nullptr;
+    // persistent surfaces
+    int64_t *sae = nullptr, *ftime = nullptr, *touch = nullptr;
+    FlowCell *fsnap = nullptr;
+    int32_t *touch_last = nullptr;
+    uint64_t *bitmap = nullptr;
+    int64_t nwords = 0;
+    uint32_t seq = 0;
+    // per-call workspace
+    int64_t cap = 0;
+    int32_t *x = nullptr, *y = nullptr, *p = nullptr;
+    uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
+    int32_t *iota = nullptr, *P = nullptr, *pos = nullptr, *prev = nullptr, *next = nullptr;
+    uint8_t *valid = nullptr;
+    FlowCell *evf = nullptr;
+    double *o_d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int32_t *o_scale = nullptr;
+    uint32_t *ctmin = nullptr, *ctmax = nullptr;
+    void *cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    int *err = nullptr;
+    unsigned long long *counters = nullptr;
+    bool profiling = false;
+    hipEvent_t ev[8] = {};
+    std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
+    farms_stats stats{};
+};
+
+namespace {
+
+template <typename T>
+int dalloc(T **ptr, size_t count) {
+    HIPCHK(hipMalloc((void **)ptr, sizeof(T) * (count ? count : 1)));
+    return FARMS_OK;
+}
+
+template <typename T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+void free_workspace(farms_handle *h) {
+    dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
+    dfree(h->iota); dfree(h->P); dfree(h->pos); dfree(h->prev); dfree(h->next);
+    dfree(h->valid); dfree(h->evf); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
+    for (auto &d : h->o_d) dfree(d);
+    dfree(h->cub_tmp);
+    h->cub_bytes = 0;
+    h->cap = 0;
+}
+
+int end_bit_for(int64_t WH) {
+    int b = 1;
+    while ((int64_t(1) << b) < WH) ++b;
+    return b;
+}
+
+int ensure_capacity(farms_handle *h, int64_t n) {
+    if (n <= h->cap) return FARMS_OK;
+    free_workspace(h);
+    const int64_t cap = n;
+    const int64_t nch = (cap + h->pool_chunk - 1) / h->pool_chunk;
+    int rc;
+    if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
+        (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
+        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->pos, cap)) ||
+        (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
+        (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
+        (rc = dalloc(&h->ctmax, nch))) {
+        free_workspace(h);
+        return rc;
+    }
+    for (auto &d : h->o_d)
+        if ((rc = dalloc(&d, cap))) { free_workspace(h); return rc; }
+    size_t bytes = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, h->pix, h->skey, h->iota, h->P, (int)cap, 0,
+                                              end_bit_for(h->WH), h->stream));
+    if ((rc = dalloc((uint8_t **)&h->cub_tmp, bytes))) { free_workspace(h); return rc; }
+    h->cub_bytes = bytes;
+    h->cap = cap;
+    return FARMS_OK;
+}
+
+int reset_surfaces(farms_handle *h) {
+    HIPCHK(hipMemsetAsync(h->sae, 0xFF, sizeof(int64_t) * h->WH, h->stream));     // -1: never visited
+    HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
+    HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->touch, 0, sizeof(int64_t) * h->WH, h->stream));      // seq 0 = never
+    HIPCHK(hipMemsetAsync(h->touch_last, 0, sizeof(int32_t) * h->WH, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->seq = 0;
+    return FARMS_OK;
+}
+
+template <int K>
+void launch_pool(const Ctx &c, int c0, int c1, uint32_t seq, hipStream_t s) {
+    const int waves = c1 - c0;
+    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), 0, s, c, c0, c1, seq);
+}
+
+typedef void (*pool_launcher)(const Ctx &, int, int, uint32_t, hipStream_t);
+pool_launcher pool_for(int K) {
+    switch (K) {
+    case 1: return launch_pool<1>;   case 2: return launch_pool<2>;   case 3: return launch_pool<3>;
+    case 4: return launch_pool<4>;   case 5: return launch_pool<5>;   case 6: return launch_pool<6>;
+    case 7: return launch_pool<7>;   case 8: return launch_pool<8>;   case 9: return launch_pool<9>;
+    case 10: return launch_pool<10>; case 11: return launch_pool<11>; case 12: return launch_pool<12>;
+    case 13: return launch_pool<13>; case 14: return launch_pool<14>; case 15: return launch_pool<15>;
+    case 16: return launch_pool<16>;
+    default: return nullptr;
+    }
+}
+
+void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s) {
+    const dim3 g(ceil_div(c1 - c0, 256)), b(256);
+    switch (fr) {
+    case 1: hipLaunchKernelGGL(k_fit<1>, g, b, 0, s, c, c0, c1, seq); break;
+    case 2: hipLaunchKernelGGL(k_fit<2>, g, b, 0, s, c, c0, c1, seq); break;
+    case 3: hipLaunchKernelGGL(k_fit<3>, g, b, 0, s, c, c0, c1, seq); break;
+    default: hipLaunchKernelGGL(k_fit<0>, g, b, 0, s, c, c0, c1, seq); break;
+    }
+}
+
+int ensure_kernel_events(farms_handle *h, size_t count) {
+    while (h->kev.size() < count) {
+        hipEvent_t ev;
+        HIPCHK(hipEventCreate(&ev));
+        h->kev.push_back(ev);
+    }
+    return FARMS_OK;
+}
+
+// The whole per-event loop for n device-resident events.
+int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
+             int64_t n64, farms_records *dout) {
+    const int n = (int)n64;
+    hipStream_t s = h->stream;
+    Ctx c{};
+    c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH;
+    c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
+    c.x = dx; c.y = dy; c.t = dt; c.p = dp;
+    c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.pos = h->pos; c.prev = h->prev; c.next = h->next;
+    c.touch = h->touch; c.touch_last = h->touch_last; c.sae = h->sae; c.fsnap = h->fsnap; c.ftime = h->ftime;
+    c.evf = h->evf; c.valid = h->valid; c.bitmap = h->bitmap; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
+    c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
+    c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
+    c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
+    if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
+    c.counters = h->counters;
+
+    const bool prof = h->profiling;
+    const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
+    if (prof) {
+        int rc = ensure_kernel_events(h, 2 * (size_t)(n_fit_chunks + n_pool_chunks));
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(h->ev[0], s));
+    }
+    // ---- prep: validate, pixel ids, sort by pixel, links
+    HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->err);
+    int herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (herr) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+    size_t bytes = h->cub_bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
+                                              end_bit_for(h->WH), s));
+    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next);
+    const int nch = ceil_div(n, h->pool_chunk);
+    hipLaunchKernelGGL(k_chunk_minmax, dim3(nch), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
+    if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
+
+    // ---- sweep 1: local plane fits
+    int fit_launches = 0;
+    for (int c0 = 0; c0 < n; c0 += h->fit_chunk) {
+        const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->fit_chunk, n);
+        const uint32_t seq = ++h->seq;
+        const dim3 g(ceil_div(c1 - c0, 256)), b(256);
+        hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches], s));
+        launch_fit(c, h->fr, c0, c1, seq, s);
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches + 1], s));
+        hipLaunchKernelGGL(k_sae_update, g, b, 0, s, c, c0, c1);
+        ++fit_launches;
+    }
+    HIPCHK(hipGetLastError());
+    if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
+
+    // ---- sweep 2: multiscale pooling
+    pool_launcher pl = pool_for(h->K);
+    int pool_launches = 0;
+    const int bm_blocks = ceil_div(h->nwords * 64, 256);
+    for (int ch = 0, c0 = 0; c0 < n; ++ch, c0 += h->pool_chunk) {
+        const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->pool_chunk, n);
+        const uint32_t seq = ++h->seq;
+        const dim3 g(ceil_div(c1 - c0, 256)), b(256);
+        hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
+        hipLaunchKernelGGL(k_bitmap, dim3(bm_blocks), dim3(256), 0, s, c, ch, seq);
+        const size_t ke = 2 * ((size_t)n_fit_chunks + pool_launches);
+        if (prof) HIPCHK(hipEventRecord(h->kev[ke], s));
+        pl(c, c0, c1, seq, s);
+        if (prof) HIPCHK(hipEventRecord(h->kev[ke + 1], s));
+        hipLaunchKernelGGL(k_flow_update, g, b, 0, s, c, c0, c1);
+        ++pool_launches;
+    }
+    HIPCHK(hipGetLastError());
+    if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
+    if (prof) {
+        HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 3, s));
+        hipLaunchKernelGGL(k_stats, dim3(1024), dim3(256), 0, s, c);
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+
+    farms_stats st{};
+    st.n_events = n;
+    st.fit_launches = fit_launches;
+    st.pool_launches = pool_launches;
+    if (prof) {
+        float a = 0, b = 0, d = 0;
+        HIPCHK(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
+        HIPCHK(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+        HIPCHK(hipEventElapsedTime(&d, h->ev[2], h->ev[3]));
+        st.ms_prep = a; st.ms_fit = b; st.ms_pool = d; st.ms_total = (double)a + b + d;
+        double kf = 0, kp = 0;
+        for (int i = 0; i < fit_launches; ++i) {
+            float v = 0;
+            HIPCHK(hipEventElapsedTime(&v, h->kev[2 * i], h->kev[2 * i + 1]));
+            kf += v;
+        }
+        for (int i = 0; i < pool_launches; ++i) {
+            float v = 0;
+            const size_t ke = 2 * ((size_t)n_fit_chunks + i);
+            HIPCHK(hipEventElapsedTime(&v, h->kev[ke], h->kev[ke + 1]));
+            kp += v;
+        }
+        st.ms_fit_kernel = kf;
+        st.ms_pool_kernel = kp;
+        unsigned long long cnt[3];
+        HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        st.n_valid = (int64_t)cnt[0];
+        st.sae_cells = (double)cnt[1];
+        st.pool_cells = (double)cnt[2];
+    }
+    h->stats = st;
+    return FARMS_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+
+extern "C" const char *farms_last_error(void) { return g_err.c_str(); }
+
+extern "C" int farms_default_params(farms_params *o) {
+    if (!o) return fail(FARMS_EINVAL, "null params");
+    std::memset(o, 0, sizeof(*o));
+    o->width = 320; o->height = 320; o->filter_size = 3; o->min_inliers = 5;  // main.cpp:21-24
+    o->window_jump = 5; o->max_window = 50;                                    // vFlow.cpp:73-74
+    return FARMS_OK;
+}
+
+extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
+    if (!prm || !out) return fail(FARMS_EINVAL, "null argument");
+    *out = nullptr;
+    if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height >= (int64_t(1) << 31))
+        return fail(FARMS_EINVAL, "sensor size out of range");
+    if (prm->window_jump <= 0 || prm->max_window < 0) return fail(FARMS_EINVAL, "bad pooling scales");
+    const int K = prm->max_window / prm->window_jump + 1;
+    // spatialPool has maxWindow slots and is indexed with .at() (vFlow.cpp:966,1025)
+    if (K > prm->max_window) return fail(FARMS_EINVAL, "more pooling scales than maxWindow (reference throws)");
+    if (K > kMaxScales) return fail(FARMS_EINVAL, "at most 16 pooling scales are supported");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(FARMS_ENODEV, "no HIP device");
+    if (prm->device < 0 || prm->device >= ndev) return fail(FARMS_ENODEV, "device ordinal out of range");
+    HIPCHK(hipSetDevice(prm->device));
+    farms_handle *h = new (std::nothrow) farms_handle();
+    if (!h) return fail(FARMS_ENOMEM, "host allocation");
+    h->prm = *prm;
+    int fs = prm->filter_size;  // vFlow.cpp:32-34
+    if (fs < 5) fs = 3;
+    if (!(fs % 2)) fs--;
+    h->fr = fs / 2;
+    h->W = prm->width; h->H = prm->height; h->WH = (int64_t)prm->width * prm->height;
+    h->J = prm->window_jump; h->M = prm->max_window; h->K = K;
+    if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
+    if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
+    h->nwords = (h->WH + 63) / 64;
+    int rc = FARMS_OK;
+    auto bail = [&](int code) { farms_destroy(h); return code; };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(FARMS_EHIP, "hipStreamCreate"));
+    for (auto &ev : h->ev)
+        if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
+    if ((rc = dalloc(&h->sae, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) || (rc = dalloc(&h->touch, h->WH)) ||
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->touch_last, h->WH)) ||
+        (rc = dalloc(&h->bitmap, h->nwords)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 4)))
+        return bail(rc);
+    if ((rc = reset_surfaces(h))) return bail(rc);
+    *out = h;
+    return FARMS_OK;
+}
+
+extern "C" int farms_destroy(farms_handle *h) {
+    if (!h) return FARMS_OK;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    free_workspace(h);
+    dfree(h->sae); dfree(h->ftime); dfree(h->touch); dfree(h->fsnap); dfree(h->touch_last);
+    dfree(h->bitmap); dfree(h->err); dfree(h->counters);
+    for (auto &ev : h->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto &ev : h->kev) (void)hipEventDestroy(ev);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return FARMS_OK;
+}
+
+extern "C" int farms_reset(farms_handle *h) {
+    if (!h) return fail(FARMS_EINVAL, "null handle");
+    HIPCHK(hipSetDevice(h->prm.device));
+    return reset_surfaces(h);
+}
+
+extern "C" int farms_set_profiling(farms_handle *h, int enable) {
+    if (!h) return fail(FARMS_EINVAL, "null handle");
+    h->profiling = enable != 0;
+    return FARMS_OK;
+}
+
+extern "C" int farms_get_stats(const farms_handle *h, farms_stats *out) {
+    if (!h || !out) return fail(FARMS_EINVAL, "null argument");
+    *out = h->stats;
+    return FARMS_OK;
+}
+
+extern "C" int farms_num_scales(const farms_handle *h) { return h ? h->K : 0; }
+
+extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
+                                    const uint32_t *d_t, const int32_t *d_p, int64_t n, farms_records *d_out) {
+    if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
+    if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
+    if (n == 0) return FARMS_OK;
+    if (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx || !d_out->vy ||
+        !d_out->r_local || !d_out->theta_local || !d_out->scale)
+        return fail(FARMS_EINVAL, "null array");
+    HIPCHK(hipSetDevice(h->prm.device));
+    int rc = ensure_capacity(h, n);
+    if (rc) return rc;
+    return run_core(h, d_x, d_y, d_t, d_p, n, d_out);
+}
+
+extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
+                             const int32_t *p, int64_t n, farms_records *out) {
+    if (!h || !out) return fail(FARMS_EINVAL, "null argument");
+    if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
+    if (n == 0) return FARMS_OK;
+    if (!x || !y || !t || !p || !out->x || !out->y || !out->t || !out->p || !out->r_true || !out->theta_true ||
+        !out->vx || !out->vy || !out->r_local || !out->theta_local || !out->scale)
+        return fail(FARMS_EINVAL, "null array");
+    HIPCHK(hipSetDevice(h->prm.device));
+    int rc = ensure_capacity(h, n);
+    if (rc) return rc;
+    hipStream_t s = h->stream;
+    HIPCHK(hipMemcpyAsync(h->x, x, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->y, y, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->t, t, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->p, p, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    farms_records d{};
+    d.r_true = h->o_d[0]; d.theta_true = h->o_d[1]; d.vx = h->o_d[2]; d.vy = h->o_d[3];
+    d.r_local = h->o_d[4]; d.theta_local = h->o_d[5]; d.scale = h->o_scale;
+    rc = run_core(h, h->x, h->y, h->t, h->p, n, &d);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out->r_true, d.r_true, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->theta_true, d.theta_true, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->vx, d.vx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->vy, d.vy, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->r_local, d.r_local, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->theta_local, d.theta_local, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out->scale, d.scale, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // x, y, t, p columns echo the inputs (vFlow.cpp:370-373)
+    for (int64_t e = 0; e < n; ++e) {
+        out->x[e] = x[e]; out->y[e] = y[e]; out->t[e] = (int32_t)t[e]; out->p[e] = p[e];
+    }
+    return FARMS_OK;
+}

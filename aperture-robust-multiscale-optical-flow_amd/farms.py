@@ -1,0 +1,332 @@
+"""Python binding of libfarms_hip.so (include/farms_hip.h) and libfarms_synth.so.
+
+Mirrors the reference's vFlowManager batch interface (/root/reference/include/
+vFlow.h:22-117): construct with (height, width, filterSize, minEvtsOnPlane),
+feed events, get the 11-column _FARMSOut_ records (src/vFlow.cpp:438).  The
+accelerated path is the HIP library; there is no CPU fallback — if the library
+or a GPU is missing, every call raises FarmsError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.join(HERE, "build")
+HIP_LIB = os.path.join(BUILD_DIR, "libfarms_hip.so")
+SYNTH_LIB = os.path.join(BUILD_DIR, "libfarms_synth.so")
+
+FARMS_OK = 0
+FARMS_EINVAL = -1
+FARMS_EHIP = -2
+FARMS_ENOMEM = -3
+FARMS_ENODEV = -4
+
+# record columns, in the order of src/vFlow.cpp:438
+COLUMNS = ("x", "y", "t", "p", "r_true", "theta_true", "vx", "vy", "r_local", "theta_local", "scale")
+INT_COLUMNS = ("x", "y", "t", "p", "scale")
+
+
+class FarmsError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"farms error {code}: {msg}")
+        self.code = code
+
+
+class FarmsParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("filter_size", ctypes.c_int32),
+        ("min_inliers", ctypes.c_int32),
+        ("window_jump", ctypes.c_int32),
+        ("max_window", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("fit_chunk", ctypes.c_int32),
+        ("pool_chunk", ctypes.c_int32),
+    ]
+
+
+class FarmsRecordsC(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in COLUMNS]
+
+
+class FarmsStats(ctypes.Structure):
+    _fields_ = [
+        ("n_events", ctypes.c_int64),
+        ("n_valid", ctypes.c_int64),
+        ("sae_cells", ctypes.c_double),
+        ("pool_cells", ctypes.c_double),
+        ("fit_launches", ctypes.c_int32),
+        ("pool_launches", ctypes.c_int32),
+        ("ms_prep", ctypes.c_double),
+        ("ms_fit", ctypes.c_double),
+        ("ms_pool", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+        ("ms_fit_kernel", ctypes.c_double),
+        ("ms_pool_kernel", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class SynthParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("n_events", ctypes.c_int64),
+        ("n_bars", ctypes.c_int32),
+        ("len_min", ctypes.c_double),
+        ("len_max", ctypes.c_double),
+        ("thick_min", ctypes.c_double),
+        ("thick_max", ctypes.c_double),
+        ("speed_min", ctypes.c_double),
+        ("speed_max", ctypes.c_double),
+        ("jitter_us", ctypes.c_int32),
+        ("noise_frac", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("t0", ctypes.c_uint32),
+        ("fixed_dir_deg", ctypes.c_double),
+    ]
+
+
+# exported symbols of include/farms_hip.h and include/farms_synth.h
+HIP_SYMBOLS = (
+    "farms_default_params", "farms_create", "farms_destroy", "farms_reset", "farms_process",
+    "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
+    "farms_last_error",
+)
+SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text")
+
+_hip = None
+_synth = None
+
+
+def _ptr(a) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def load_hip_library() -> ctypes.CDLL:
+    """Load the HIP library; raise if it has not been built (no fallback)."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    if not os.path.exists(HIP_LIB):
+        raise FarmsError(FARMS_ENODEV, f"{HIP_LIB} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(HIP_LIB)
+    lib.farms_last_error.restype = ctypes.c_char_p
+    for name in HIP_SYMBOLS:
+        if name != "farms_last_error":
+            getattr(lib, name).restype = ctypes.c_int
+    lib.farms_process.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
+    lib.farms_process_device.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
+    _hip = lib
+    return lib
+
+
+def load_synth_library() -> ctypes.CDLL:
+    global _synth
+    if _synth is not None:
+        return _synth
+    if not os.path.exists(SYNTH_LIB):
+        raise FarmsError(FARMS_ENODEV, f"{SYNTH_LIB} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(SYNTH_LIB)
+    lib.farms_synth_generate.restype = ctypes.c_int64
+    lib.farms_synth_generate.argtypes = [ctypes.c_void_p] * 5
+    lib.farms_synth_write_text.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64]
+    _synth = lib
+    return lib
+
+
+def _check(lib, rc: int) -> None:
+    if rc != FARMS_OK:
+        raise FarmsError(rc, lib.farms_last_error().decode(errors="replace"))
+
+
+# ---------------------------------------------------------------------------
+# events and records
+
+
+@dataclass
+class Events:
+    """An event stream: x, y (int32), t (uint32, absolute us), p (int32, +-1)."""
+
+    x: np.ndarray
+    y: np.ndarray
+    t: np.ndarray
+    p: np.ndarray
+
+    def __len__(self) -> int:
+        return int(self.x.shape[0])
+
+    def head(self, n: int) -> "Events":
+        return Events(self.x[:n].copy(), self.y[:n].copy(), self.t[:n].copy(), self.p[:n].copy())
+
+    def relative(self) -> tuple:
+        """Host prologue of runFileCopy: t - t0 as uint32 (vFlow.cpp:194, 240-241)
+        and polarity clamped to >= 0 (vFlow.cpp:245-247)."""
+        t0 = np.uint32(self.t[0]) if len(self) else np.uint32(0)
+        t_rel = (self.t.astype(np.uint32) - t0).astype(np.uint32)
+        p = np.maximum(self.p, 0).astype(np.int32)
+        return (np.ascontiguousarray(self.x, dtype=np.int32), np.ascontiguousarray(self.y, dtype=np.int32),
+                np.ascontiguousarray(t_rel), np.ascontiguousarray(p))
+
+
+class Records:
+    """SoA of the 11 output columns (vFlow.cpp:438)."""
+
+    def __init__(self, n: int):
+        self.n = n
+        for name in COLUMNS:
+            setattr(self, name, np.zeros(n, dtype=np.int32 if name in INT_COLUMNS else np.float64))
+
+    def as_c(self) -> FarmsRecordsC:
+        return FarmsRecordsC(*[getattr(self, name).ctypes.data for name in COLUMNS])
+
+    @property
+    def valid(self) -> np.ndarray:
+        """Validity gate of vFlow.cpp:315 as seen in the output: RLocal > 0
+        (an event that passes the gate has RLocal = sqrt(Vx^2 + Vy^2) > 0)."""
+        return self.r_local > 0
+
+    def to_text(self) -> str:
+        """The _FARMSOut_ lines with ostream defaults (%g, 6 significant digits)."""
+        lines = []
+        for i in range(self.n):
+            lines.append("%d %d %d %d %s %s %s %s %s %s %d" % (
+                self.x[i], self.y[i], self.t[i], self.p[i],
+                *("%g" % getattr(self, c)[i] for c in ("r_true", "theta_true", "vx", "vy", "r_local", "theta_local")),
+                self.scale[i]))
+        return "\n".join(lines) + ("\n" if lines else "")
+
+
+# ---------------------------------------------------------------------------
+# synthetic streams
+
+
+def synth_params(config: int, n_events: int | None = None) -> SynthParams:
+    lib = load_synth_library()
+    p = SynthParams()
+    if lib.farms_synth_preset(int(config), ctypes.byref(p)) != 0:
+        raise ValueError(f"unknown synthetic configuration {config}")
+    if n_events is not None:
+        p.n_events = int(n_events)
+    return p
+
+
+def synth_generate(params: SynthParams) -> Events:
+    lib = load_synth_library()
+    n = int(params.n_events)
+    x = np.zeros(n, np.int32)
+    y = np.zeros(n, np.int32)
+    t = np.zeros(n, np.uint32)
+    p = np.zeros(n, np.int32)
+    got = lib.farms_synth_generate(ctypes.byref(params), _ptr(x), _ptr(y), _ptr(t), _ptr(p))
+    if got != n:
+        raise RuntimeError(f"farms_synth_generate returned {got}")
+    return Events(x, y, t, p)
+
+
+def synth_config(config: int, n_events: int | None = None) -> Events:
+    return synth_generate(synth_params(config, n_events))
+
+
+def write_events_text(path: str, ev: Events) -> None:
+    lib = load_synth_library()
+    x, y = np.ascontiguousarray(ev.x, np.int32), np.ascontiguousarray(ev.y, np.int32)
+    t, p = np.ascontiguousarray(ev.t, np.uint32), np.ascontiguousarray(ev.p, np.int32)
+    if lib.farms_synth_write_text(path.encode(), _ptr(x), _ptr(y), _ptr(t), _ptr(p), len(ev)) != 0:
+        raise OSError(f"cannot write {path}")
+
+
+# ---------------------------------------------------------------------------
+# the accelerated path
+
+
+class FlowManager:
+    """GPU counterpart of vFlowManager's batch path (vFlow.h:100,104).
+
+    FlowManager(height, width, filter_size, min_evts_on_plane) — argument order
+    of the reference constructor.  process() runs the per-event loop of
+    runFileCopy on events whose time is already relative to t0 and whose
+    polarity is already clamped (see Events.relative()).  State persists across
+    calls.
+    """
+
+    def __init__(self, height: int = 320, width: int = 320, filter_size: int = 3, min_evts_on_plane: int = 5,
+                 window_jump: int = 5, max_window: int = 50, device: int = 0, fit_chunk: int = 0,
+                 pool_chunk: int = 0):
+        self._lib = load_hip_library()
+        prm = FarmsParams()
+        _check(self._lib, self._lib.farms_default_params(ctypes.byref(prm)))
+        prm.width, prm.height = int(width), int(height)
+        prm.filter_size, prm.min_inliers = int(filter_size), int(min_evts_on_plane)
+        prm.window_jump, prm.max_window = int(window_jump), int(max_window)
+        prm.device, prm.fit_chunk, prm.pool_chunk = int(device), int(fit_chunk), int(pool_chunk)
+        self.params = prm
+        h = ctypes.c_void_p()
+        _check(self._lib, self._lib.farms_create(ctypes.byref(prm), ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.farms_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def num_scales(self) -> int:
+        return int(self._lib.farms_num_scales(self._h))
+
+    def reset(self) -> None:
+        _check(self._lib, self._lib.farms_reset(self._h))
+
+    def set_profiling(self, on: bool) -> None:
+        _check(self._lib, self._lib.farms_set_profiling(self._h, 1 if on else 0))
+
+    def stats(self) -> dict:
+        st = FarmsStats()
+        _check(self._lib, self._lib.farms_get_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def process(self, x, y, t_rel, p) -> Records:
+        x = np.ascontiguousarray(x, dtype=np.int32)
+        y = np.ascontiguousarray(y, dtype=np.int32)
+        t_rel = np.ascontiguousarray(t_rel, dtype=np.uint32)
+        p = np.ascontiguousarray(p, dtype=np.int32)
+        n = int(x.shape[0])
+        if not (y.shape[0] == t_rel.shape[0] == p.shape[0] == n):
+            raise ValueError("x, y, t, p must have the same length")
+        rec = Records(n)
+        out = rec.as_c()
+        _check(self._lib, self._lib.farms_process(self._h, _ptr(x), _ptr(y), _ptr(t_rel), _ptr(p), n,
+                                                  ctypes.byref(out)))
+        return rec
+
+    def process_events(self, ev: Events) -> Records:
+        return self.process(*ev.relative())
+
+    def process_device(self, x, y, t_rel, p, out: dict) -> None:
+        """Device-resident variant: torch tensors (int32 x/y/p, int32 view of the
+        uint32 t) on this handle's device; `out` maps column name -> tensor
+        (float64 for the six float columns, int32 for scale)."""
+        n = int(x.shape[0])
+        rec = FarmsRecordsC(0, 0, 0, 0, *[out[c].data_ptr() for c in COLUMNS[4:]])
+        _check(self._lib, self._lib.farms_process_device(
+            self._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+            ctypes.c_void_p(t_rel.data_ptr()), ctypes.c_void_p(p.data_ptr()), n, ctypes.byref(rec)))

@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""bench.py — FARMS_Flow batch hot path on MI355X.
+
+Metric (BASELINE.json): Mevents/s (and % of the HBM roofline) at 1/2/4/8 GPUs.
+Workload at N=1: BASELINE config 3 — synthetic 1280x720 DVS-shape stream, 50M
+events, filtersize 5, inlierCheck 5 (the north_star's headline configuration).
+A step = one full pass of the hot path (surfaces reset + every event through
+local fit and multiscale pooling) over the whole resident stream.
+
+Multi-GPU (torchrun, one process per GPU): spatial x-strips, weak scaling — see
+DESIGN.md §6.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "aperture-robust-multiscale-optical-flow_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+import farms  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720), 4: (1280, 720), 5: (1280, 720)}
+FILTER = {1: 3, 2: 5, 3: 5, 4: 7, 5: 7}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--events", type=int, default=0, help="override the stream length")
+    ap.add_argument("--fit-chunk", type=int, default=0)
+    ap.add_argument("--pool-chunk", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=400_000, help="events in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(ev, width, height, fs, jump, maxw, n_sample):
+    """Oracle ("port": single-thread C restatement, -O2) on the first n_sample
+    events of the same stream."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleFlow
+
+    sample = ev.head(min(n_sample, len(ev)))
+    x, y, t, p = sample.relative()
+    of = OracleFlow(height, width, fs, 5, jump, maxw)
+    t0 = time.perf_counter()
+    of.process(x, y, t, p)
+    dt = time.perf_counter() - t0
+    return {"value": len(sample) / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
+            "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local_rank)
+
+    cfg = args.config
+    W, H = SENSOR[cfg]
+    fs = FILTER[cfg]
+    jump, maxw = (25, 50) if cfg == 5 else (5, 50)
+    sp = farms.synth_params(cfg, args.events or None)
+    if cfg in (4, 5):
+        sp.n_events = args.events or 50_000_000  # per-GPU share fixed (weak scaling)
+    # weak scaling: every rank owns a full-size stream of its own (independent seed)
+    sp.seed = int(sp.seed) + 0x1000 * rank
+    ev = farms.synth_generate(sp)
+    n = len(ev)
+    x, y, t, p = ev.relative()
+    dx = torch.from_numpy(x).to(dev)
+    dy = torch.from_numpy(y).to(dev)
+    dt_ = torch.from_numpy(t.view(np.int32)).to(dev)
+    dp = torch.from_numpy(p).to(dev)
+    out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+           for c in farms.COLUMNS[4:]}
+    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=local_rank,
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk)
+    torch.cuda.synchronize()
+
+    def step():
+        fm.reset()
+        fm.process_device(dx, dy, dt_, dp, out)
+
+    for _ in range(args.warmup):
+        step()
+    fm.set_profiling(True)
+    stats = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stats.append(fm.stats())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        nn = torch.tensor([n], device=dev, dtype=torch.float64)
+        dist.all_reduce(nn)
+        total_events = float(nn.item())
+    else:
+        total_events = float(n)
+
+    ms_step = elapsed / args.steps * 1e3
+    value = total_events * args.steps / elapsed / 1e6
+    st = stats[-1]
+    pool_ms = sum(s["ms_pool_kernel"] for s in stats) / len(stats)
+    pool_launches = st["pool_launches"]
+    alg_bytes = 20.0 * st["pool_cells"]  # 20 B per pooled cell of a valid event
+    achieved = alg_bytes / (pool_ms / 1e3) / 1e9 if pool_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_pool", "launches_per_step": pool_launches,
+                "avg_launch_us": round(pool_ms * 1e3 / max(pool_launches, 1), 2)}
+    line = {
+        "metric": "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref",
+        "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"BASELINE config {cfg}: {W}x{H} synthetic moving-bars stream, "
+                               f"{n} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
+                   "events_per_gpu": n, "width": W, "height": H, "filtersize": fs,
+                   "parallelism": f"{world} independent stream(s)" if world > 1 else "1 GPU"},
+        "roofline": roofline,
+        "detail": {"valid_frac": round(st["n_valid"] / max(st["n_events"], 1), 4),
+                   "ms_prep": round(st["ms_prep"], 3), "ms_fit_sweep": round(st["ms_fit"], 3),
+                   "ms_pool_sweep": round(st["ms_pool"], 3), "ms_pool_kernel": round(pool_ms, 3),
+                   "ms_fit_kernel": round(st["ms_fit_kernel"], 3),
+                   "dense_equiv_bytes_per_event": round(alg_bytes / max(n, 1), 1)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(ev, W, H, fs, jump, maxw, args.cpu_sample)
+    fm.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * farms_hip.h — C ABI of libfarms_hip.so, the MI355X (gfx950) drop-in for the
+ * FARMS_Flow batch hot path.
+ *
+ * The reference has no plugin registry or FFI: its boundary for this path is the
+ * C++ class vFlowManager (/root/reference/include/vFlow.h:22-117), whose batch
+ * method runFileCopy (/root/reference/src/vFlow.cpp:111-460) parses a text file,
+ * runs the per-event loop (vFlow.cpp:223-414) and writes the _FARMSOut_ file.
+ * This ABI replaces exactly that per-event loop; parsing, t0 subtraction,
+ * polarity clamping, timing and the text writer stay in the host C++ mirror of
+ * vFlowManager (host/vFlow.cpp), see INTEGRATION.md.
+ *
+ * Plain pointers and sizes only.  One handle per host thread; a handle owns one
+ * HIP stream and the persistent sensor surfaces, so a stream of events may be fed
+ * through several farms_process calls with results identical to one call.
+ */
+#ifndef FARMS_HIP_H
+#define FARMS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define FARMS_OK 0
+#define FARMS_EINVAL (-1)  /* bad parameter, or an event outside the W x H sensor */
+#define FARMS_EHIP (-2)    /* a HIP runtime call failed (message in farms_last_error) */
+#define FARMS_ENOMEM (-3)  /* device or host allocation failed */
+#define FARMS_ENODEV (-4)  /* no usable gfx950 device */
+
+typedef struct farms_handle farms_handle;
+
+/* Constructor arguments of vFlowManager::vFlowManager(height, width, filterSize,
+ * minEvtsOnPlane, fileName) (vFlow.h:100, vFlow.cpp:22-108), plus the two
+ * constants the reference hard-codes at vFlow.cpp:73-74 (windowJump = 5,
+ * maxWindow = 50; exposed for BASELINE config 5's 3-scale run) and placement. */
+typedef struct {
+    int32_t width;        /* --width  (vFlow.cpp:28) */
+    int32_t height;       /* --height (vFlow.cpp:27) */
+    int32_t filter_size;  /* --filtersize, normalised as vFlow.cpp:32-36 */
+    int32_t min_inliers;  /* --inlierCheck = minEvtsOnPlane (vFlow.cpp:38) */
+    int32_t window_jump;  /* pooling scale step, reference 5 */
+    int32_t max_window;   /* largest pooling radius, reference 50 */
+    int32_t device;       /* HIP device ordinal */
+    int32_t fit_chunk;    /* events per local-fit chunk, 0 = default */
+    int32_t pool_chunk;   /* events per pooling chunk, 0 = default */
+} farms_params;
+
+/* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA
+ * form: x y t p RTrue ThetaTrue Vx Vy RLocal ThetaLocal scale.  For
+ * farms_process these are host arrays of length n; for farms_process_device
+ * they are device arrays (x, y, t, p may be NULL there: they equal the inputs). */
+typedef struct {
+    int32_t *x, *y, *t, *p;
+    double *r_true, *theta_true;
+    double *vx, *vy;
+    double *r_local, *theta_local;
+    int32_t *scale;
+} farms_records;
+
+/* Counters of the most recent farms_process* call. */
+typedef struct {
+    int64_t n_events;
+    int64_t n_valid;         /* events that passed the validity gate (vFlow.cpp:315) */
+    double sae_cells;        /* sum over events of U_loc */
+    double pool_cells;       /* sum over valid events of U_pool */
+    int32_t fit_launches, pool_launches;
+    /* kernel time, ms, from HIP events on the handle's stream; filled only when
+     * profiling is enabled (farms_set_profiling) */
+    double ms_prep, ms_fit, ms_pool, ms_total;  /* phases: prep / fit sweep / pool sweep */
+    double ms_fit_kernel;   /* sum of k_fit launch durations */
+    double ms_pool_kernel;  /* sum of k_pool launch durations */
+} farms_stats;
+
+/* vFlowManager ctor defaults: 320 x 320, filter 3, 5 inliers (main.cpp:21-24),
+ * windowJump 5, maxWindow 50 (vFlow.cpp:73-74), device 0. */
+int farms_default_params(farms_params *out);
+
+int farms_create(const farms_params *params, farms_handle **out);
+int farms_destroy(farms_handle *h);
+
+/* Forget every event seen so far (fresh surfaces, as a new vFlowManager). */
+int farms_reset(farms_handle *h);
+
+/* Run the per-event loop of runFileCopy (vFlow.cpp:223-414) over n events in
+ * stream order.  t_rel is T - t0 as uint32 (vFlow.cpp:240-241); p is the
+ * polarity already clamped to >= 0 (vFlow.cpp:245-247) and is only echoed.
+ * Host pointers.  Synchronous. */
+int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t_rel,
+                  const int32_t *p, int64_t n, farms_records *out);
+
+/* Same with device-resident inputs and outputs (no PCIe traffic).  Synchronous
+ * with respect to the handle's stream. */
+int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
+                         const uint32_t *d_t_rel, const int32_t *d_p, int64_t n,
+                         farms_records *d_out);
+
+/* Record HIP events around every kernel of the next calls (per-kernel times in
+ * farms_stats).  0 = off (default). */
+int farms_set_profiling(farms_handle *h, int enable);
+int farms_get_stats(const farms_handle *h, farms_stats *out);
+
+/* Number of pooling scales, floor(max_window / window_jump) + 1. */
+int farms_num_scales(const farms_handle *h);
+
+/* Thread-local message for the last non-OK status. */
+const char *farms_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

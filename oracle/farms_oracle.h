@@ -1,0 +1,54 @@
+/*
+ * farms_oracle.h — CPU restatement of the FARMS_Flow batch hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the HIP path and the
+ * timed CPU baseline ("port") of bench.py.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product library
+ * (libfarms_hip.so) never links or calls it.
+ *
+ * PARITY STATUS: "parity unpinned".  The reference has no tests, fixtures or
+ * golden vectors, and it cannot be built in this image: it needs
+ * Eigen3 and Boost, neither of which is present, and building it
+ * against stand-in headers is not allowed.  The restatement below follows the
+ * reference source line by line (citations are /root/reference paths) and
+ * restates Eigen 3.4's evaluation order for the three Eigen calls on the path.
+ * It is pinned only by analytic known-answer tests (tests/test_oracle_kat.py).
+ */
+#ifndef FARMS_ORACLE_H
+#define FARMS_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct farms_oracle farms_oracle;
+
+/* Mirrors vFlowManager::vFlowManager (src/vFlow.cpp:22-108) plus the two
+ * constants the reference hard-codes (windowJump/maxWindow, vFlow.cpp:73-74),
+ * exposed so the 3-scale configuration (BASELINE config 5) can be checked.
+ * Returns 0 on success, a negative code on bad parameters. */
+int farms_oracle_create(int width, int height, int filter_size, int min_inliers,
+                        int window_jump, int max_window, farms_oracle **out);
+void farms_oracle_destroy(farms_oracle *o);
+
+/* Per-event loop of runFileCopy (src/vFlow.cpp:223-414) over events whose time
+ * is already relative (t - t0, uint32) and whose polarity is already clamped,
+ * i.e. what the host hands to the C ABI.  State persists across calls, so a
+ * stream may be fed in pieces.  Output arrays receive one record per event, in
+ * input order, exactly the 11 columns written at src/vFlow.cpp:438.
+ * Returns 0, or -2 if an event lies outside the W x H sensor. */
+int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
+                         const uint32_t *t_rel, const int32_t *p, int64_t n,
+                         int32_t *out_x, int32_t *out_y, int32_t *out_t, int32_t *out_p,
+                         double *r_true, double *theta_true, double *vx, double *vy,
+                         double *r_local, double *theta_local, int32_t *scale);
+
+/* Number of pooling scales (floor(maxWindow/windowJump) + 1). */
+int farms_oracle_num_scales(const farms_oracle *o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,77 @@
+"""ctypes binding of the CPU oracle (oracle/farms_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline — never by the
+product path.  Parity status: "parity unpinned" (see farms_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libfarms_oracle.so")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        lib.farms_oracle_process.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64] + [ctypes.c_void_p] * 11
+        lib.farms_oracle_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_void_p]
+        lib.farms_oracle_destroy.argtypes = [ctypes.c_void_p]
+        lib.farms_oracle_num_scales.argtypes = [ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+class OracleFlow:
+    """CPU vFlowManager batch loop: OracleFlow(height, width, filter_size, min_evts)."""
+
+    def __init__(self, height=320, width=320, filter_size=3, min_evts_on_plane=5, window_jump=5, max_window=50):
+        self._lib = load()
+        h = ctypes.c_void_p()
+        rc = self._lib.farms_oracle_create(int(width), int(height), int(filter_size), int(min_evts_on_plane),
+                                           int(window_jump), int(max_window), ctypes.byref(h))
+        if rc != 0:
+            raise ValueError(f"farms_oracle_create failed ({rc})")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            self._lib.farms_oracle_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process(self, x, y, t_rel, p):
+        """Returns a dict of the 11 output columns."""
+        from_cols = ("x", "y", "t", "p", "r_true", "theta_true", "vx", "vy", "r_local", "theta_local", "scale")
+        x = np.ascontiguousarray(x, np.int32)
+        y = np.ascontiguousarray(y, np.int32)
+        t_rel = np.ascontiguousarray(t_rel, np.uint32)
+        p = np.ascontiguousarray(p, np.int32)
+        n = int(x.shape[0])
+        out = {c: np.zeros(n, np.int32 if c in ("x", "y", "t", "p", "scale") else np.float64) for c in from_cols}
+        ptr = lambda a: ctypes.c_void_p(a.ctypes.data)
+        rc = self._lib.farms_oracle_process(self._h, ptr(x), ptr(y), ptr(t_rel), ptr(p), n,
+                                            *[ptr(out[c]) for c in from_cols])
+        if rc != 0:
+            raise ValueError(f"farms_oracle_process failed ({rc})")
+        return out

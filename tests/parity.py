@@ -1,0 +1,86 @@
+"""Record comparison used by the parity tests.
+
+Bar (north_star): x/y/t/p and the validity flag bit-exact;
+RTrue/RLocal relative error <= 1e-4; ThetaTrue/ThetaLocal wrap-aware
+|dtheta| <= 1e-4 rad; scale-column mismatches counted and reported.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+REL_TOL = 1e-4
+ANG_TOL = 1e-4
+
+
+def _get(rec, name):
+    return rec[name] if isinstance(rec, dict) else getattr(rec, name)
+
+
+def wrap_diff(a, b):
+    d = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)) % (2 * np.pi)
+    return np.minimum(d, 2 * np.pi - d)
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = np.maximum(np.abs(b), 1e-300)
+    err = np.abs(a - b) / den
+    both_zero = (a == 0) & (b == 0)
+    both_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
+    both_nan = np.isnan(a) & np.isnan(b)
+    err[both_zero | both_inf | both_nan] = 0.0
+    return err
+
+
+def compare(gpu, ref) -> dict:
+    """Return a report dict; report['ok'] is the pass/fail of the bar."""
+    rep = {}
+    n = len(_get(ref, "x"))
+    rep["n"] = n
+    for c in ("x", "y", "t", "p"):
+        rep[f"{c}_mismatch"] = int(np.count_nonzero(_get(gpu, c) != _get(ref, c)))
+    vg = _get(gpu, "r_local") > 0
+    vr = _get(ref, "r_local") > 0
+    rep["valid_ref"] = int(vr.sum())
+    rep["valid_mismatch"] = int(np.count_nonzero(vg != vr))
+    both = vg & vr
+    for c in ("r_true", "r_local"):
+        e = rel_err(_get(gpu, c)[both], _get(ref, c)[both])
+        rep[f"{c}_max_rel"] = float(e.max()) if e.size else 0.0
+    for c in ("theta_true", "theta_local"):
+        e = wrap_diff(_get(gpu, c)[both], _get(ref, c)[both])
+        e[np.isnan(_get(gpu, c)[both]) & np.isnan(_get(ref, c)[both])] = 0
+        rep[f"{c}_max_abs"] = float(np.nanmax(e)) if e.size else 0.0
+    # raw local flow vector, printed for invalid events too (vFlow.cpp:394-395).
+    # Error relative to |v|: near theta = +-pi/2 one component is speed*cos(~pi/2)
+    # ~ 1e-16*speed, where a 1-ulp change of the angle is a 100% change of that
+    # component but 1e-16 of the vector.
+    gx, gy = np.asarray(_get(gpu, "vx"), np.float64), np.asarray(_get(gpu, "vy"), np.float64)
+    rx, ry = np.asarray(_get(ref, "vx"), np.float64), np.asarray(_get(ref, "vy"), np.float64)
+    fin = np.isfinite(rx) & np.isfinite(ry)
+    same_nonfinite = (~fin) & (((gx == rx) | (np.isnan(gx) & np.isnan(rx))) & ((gy == ry) | (np.isnan(gy) & np.isnan(ry))))
+    with np.errstate(invalid="ignore", over="ignore"):
+        norm = np.hypot(rx, ry)
+        err = np.where(norm > 0, np.hypot(gx - rx, gy - ry) / np.where(norm > 0, norm, 1.0), np.hypot(gx, gy))
+    err = np.where(fin, err, np.where(same_nonfinite, 0.0, np.inf))
+    rep["v_max_rel"] = float(err.max()) if err.size else 0.0
+    rep["scale_mismatch"] = int(np.count_nonzero(_get(gpu, "scale")[both] != _get(ref, "scale")[both]))
+    ok = all(rep[f"{c}_mismatch"] == 0 for c in ("x", "y", "t", "p")) and rep["valid_mismatch"] == 0
+    ok = ok and rep["r_true_max_rel"] <= REL_TOL and rep["r_local_max_rel"] <= REL_TOL
+    ok = ok and rep["theta_true_max_abs"] <= ANG_TOL and rep["theta_local_max_abs"] <= ANG_TOL
+    ok = ok and rep["v_max_rel"] <= REL_TOL
+    rep["ok"] = bool(ok)
+    return rep
+
+
+def bitwise_equal(a, b) -> bool:
+    cols = ("x", "y", "t", "p", "r_true", "theta_true", "vx", "vy", "r_local", "theta_local", "scale")
+    for c in cols:
+        u, v = np.asarray(_get(a, c)), np.asarray(_get(b, c))
+        if u.dtype.kind == "f":
+            if not np.array_equal(u.view(np.int64), v.view(np.int64)):
+                return False
+        elif not np.array_equal(u, v):
+            return False
+    return True

@@ -1,0 +1,154 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Oracle status: "parity unpinned" (no reference fixtures exist; the reference
+cannot be built here — see DESIGN.md §4).  Tolerances: tests/parity.py
+(indices / polarity / validity bit-exact, r and theta within 1e-4).
+"""
+import numpy as np
+import pytest
+
+import farms
+from oracle import OracleFlow
+from parity import bitwise_equal, compare
+
+pytestmark = pytest.mark.gpu
+
+SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720)}
+
+
+def run_pair(ev, width, height, fs, inl=5, jump=5, maxw=50, **kw):
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(height, width, fs, inl, window_jump=jump, max_window=maxw, **kw) as fm:
+        g = fm.process(x, y, t, p)
+    r = OracleFlow(height, width, fs, inl, jump, maxw).process(x, y, t, p)
+    return g, r
+
+
+def assert_parity(g, r, max_scale_frac=2e-3):
+    rep = compare(g, r)
+    print(rep)
+    assert rep["ok"], rep
+    assert rep["scale_mismatch"] <= max(1, max_scale_frac * max(rep["valid_ref"], 1)), rep
+    return rep
+
+
+@pytest.mark.parametrize("cfg,n,fs", [(1, 100_000, 3), (2, 300_000, 5), (3, 250_000, 5), (3, 120_000, 7)])
+def test_configs_vs_oracle(cfg, n, fs):
+    W, H = SENSOR[cfg]
+    ev = farms.synth_config(cfg, n)
+    g, r = run_pair(ev, W, H, fs)
+    rep = assert_parity(g, r)
+    assert rep["valid_ref"] > n // 20  # the stream really exercises pooling
+
+
+def test_three_scales_vs_oracle():
+    """BASELINE config 5 shape: fs=7 with scales {0,25,50}."""
+    ev = farms.synth_config(5, 120_000)
+    g, r = run_pair(ev, 1280, 720, 7, jump=25, maxw=50)
+    assert_parity(g, r)
+    assert set(np.unique(g.scale)) <= {0, 25, 50}
+
+
+def test_chunking_is_bitwise_invariant():
+    ev = farms.synth_config(3, 200_000)
+    x, y, t, p = ev.relative()
+    outs = []
+    for fc, pc in [(0, 0), (777, 313), (50_000, 4096), (1 << 22, 1 << 20)]:
+        with farms.FlowManager(720, 1280, 5, 5, fit_chunk=fc, pool_chunk=pc) as fm:
+            outs.append(fm.process(x, y, t, p))
+    for o in outs[1:]:
+        assert bitwise_equal(outs[0], o)
+
+
+def test_streaming_split_equals_one_call():
+    ev = farms.synth_config(2, 150_000)
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(320, 320, 5, 5) as fm:
+        whole = fm.process(x, y, t, p)
+    with farms.FlowManager(320, 320, 5, 5) as fm:
+        parts = [fm.process(x[a:b], y[a:b], t[a:b], p[a:b]) for a, b in [(0, 1), (1, 40_000), (40_000, 40_001),
+                                                                       (40_001, 150_000)]]
+    cat = {c: np.concatenate([getattr(q, c) for q in parts]) for c in farms.COLUMNS}
+    assert bitwise_equal(whole, cat)
+
+
+def test_reset_restarts_the_stream():
+    ev = farms.synth_config(1, 20_000)
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(128, 128, 3, 5) as fm:
+        a = fm.process(x, y, t, p)
+        fm.reset()
+        b = fm.process(x, y, t, p)
+    assert bitwise_equal(a, b)
+
+
+def test_unsorted_timestamps_vs_oracle():
+    """The reference never assumes time order: wrapped / out-of-order stamps,
+    future stamps (MAXSTAMP branch, vFlow.cpp:897-902 and 1229-1230)."""
+    rng = np.random.default_rng(7)
+    ev = farms.synth_config(2, 60_000)
+    x, y, t, p = ev.relative()
+    t = t.astype(np.int64)
+    swap = rng.random(t.shape[0]) < 0.05
+    t[swap] = rng.integers(0, int(t.max()) + 1, swap.sum())
+    t = t.astype(np.uint32)
+    with farms.FlowManager(320, 320, 5, 5) as fm:
+        g = fm.process(x, y, t, p)
+    r = OracleFlow(320, 320, 5, 5).process(x, y, t, p)
+    assert_parity(g, r)
+
+
+def test_edges_hot_pixel_and_filter_sizes():
+    rng = np.random.default_rng(11)
+    W, H = 64, 48
+    n = 30_000
+    x = rng.integers(0, W, n).astype(np.int32)
+    y = rng.integers(0, H, n).astype(np.int32)
+    # corners, borders and one hot pixel firing a long burst
+    x[:400] = rng.choice([0, W - 1], 400)
+    y[400:800] = rng.choice([0, H - 1], 400)
+    x[5000:9000] = 17
+    y[5000:9000] = 9
+    t = np.sort(rng.integers(0, 2_000_000, n)).astype(np.uint32)
+    t[6000:6100] = t[6000]  # equal stamps
+    p = rng.integers(0, 2, n).astype(np.int32)
+    for fs, inl in [(1, 5), (2, 3), (4, 5), (5, 0), (6, 7), (7, 4), (9, 10)]:
+        with farms.FlowManager(H, W, fs, inl) as fm:
+            g = fm.process(x, y, t, p)
+        r = OracleFlow(H, W, fs, inl).process(x, y, t, p)
+        assert_parity(g, r)
+
+
+def test_tall_sensor_and_tiny_sensor():
+    rng = np.random.default_rng(3)
+    for W, H in [(40, 200), (5, 5), (3, 7)]:
+        n = 8000
+        x = rng.integers(0, W, n).astype(np.int32)
+        y = rng.integers(0, H, n).astype(np.int32)
+        t = np.sort(rng.integers(0, 400_000, n)).astype(np.uint32)
+        p = np.ones(n, np.int32)
+        with farms.FlowManager(H, W, 3, 3) as fm:
+            g = fm.process(x, y, t, p)
+        r = OracleFlow(H, W, 3, 3).process(x, y, t, p)
+        assert_parity(g, r)
+
+
+def test_empty_and_single_event():
+    with farms.FlowManager(320, 320, 3, 5) as fm:
+        e = fm.process(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.uint32), np.zeros(0, np.int32))
+        assert e.n == 0
+        one = fm.process(np.array([5], np.int32), np.array([6], np.int32), np.array([0], np.uint32),
+                         np.array([1], np.int32))
+    assert one.x[0] == 5 and one.y[0] == 6 and one.r_local[0] == 0 and one.scale[0] == 0
+
+
+def test_out_of_sensor_event_is_rejected():
+    with farms.FlowManager(32, 32, 3, 5) as fm:
+        with pytest.raises(farms.FarmsError) as ei:
+            fm.process(np.array([1, 32], np.int32), np.array([1, 1], np.int32), np.array([0, 1], np.uint32),
+                       np.array([1, 1], np.int32))
+        assert ei.value.code == farms.FARMS_EINVAL
+        # the handle stays usable
+        ok = fm.process(np.array([1], np.int32), np.array([1], np.int32), np.array([0], np.uint32),
+                        np.array([1], np.int32))
+        assert ok.n == 1

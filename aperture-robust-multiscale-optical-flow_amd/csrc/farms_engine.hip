@@ -58,7 +58,7 @@ int fail(int code, const std::string &msg) {
 constexpr double kMaxStamp = 4294967296.0;  // vFlow.h:27
 constexpr double kTsToSec = 1e-6;           // vFlow.h:28
 constexpr double kKillUs = 500.0;           // vFlow.cpp:961
-constexpr int kDefaultFitChunk = 1 << 20;
+constexpr int kDefaultFitChunk = 1 << 18;
 constexpr int kDefaultPoolChunk = 1 << 15;
 constexpr int kMaxScales = 16;
 
@@ -71,46 +71,89 @@ struct __attribute__((aligned(32))) FlowCell {
     uint32_t pad;
 };
 
+// SAE cell (x-major, 32 B, two 16-B loads): snapshot of the SAE at chunk start
+// plus the first two events of the current chunk at this pixel, inline, so
+// "stamp as of e" is resolved without pointer chasing unless the pixel fired
+// three or more times in the chunk (a bar's ON/OFF pair is the common case).
+// tag: bit31 = snapshot visited, bits 0..30 = seq of the chunk that last touched
+// the pixel.  e1m: first in-chunk event id, bit31 = more than one in-chunk event.
+// e2m: second in-chunk event id, bit31 = more than two (then tpos[] bounds the
+// pixel's run in P and the out-of-line search resolves it).
+struct __attribute__((aligned(16))) SaeCell {
+    uint32_t tag;
+    uint32_t e1m;
+    uint32_t t1;
+    uint32_t tsnap;
+    uint32_t e2m;
+    uint32_t t2;
+    uint32_t pad0, pad1;
+};
+
+// Pooling candidate: one cell of the per-chunk bitmap, its flow state before
+// the chunk (snap) and after its first in-chunk event (one).  Split into a
+// 16-B header read by every scan and a 48-B payload read only for contributors.
+constexpr uint32_t kCandMore = 0x80000000u;     // > 1 event at the cell in the chunk
+constexpr uint32_t kCandSnapOk = 0x40000000u;   // L_snap > 0
+constexpr uint32_t kCandOneOk = 0x20000000u;    // L1 > 0
+constexpr uint32_t kCandLinMask = 0x1FFFFFFFu;  // x-major cell index (W*H < 2^29)
+struct __attribute__((aligned(16))) CandHdr {
+    uint32_t lin;  // cell index | flags above
+    int32_t e1;    // first in-chunk event at the cell, INT_MAX if untouched
+    uint32_t t_snap, t1;
+};
+struct CandVal {
+    double L_snap, Lc_snap, Ls_snap;
+    double L1, Lc1, Ls1;
+};
+
+constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
+constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
+
 struct Ctx {
     int W, H, n;
     int64_t WH;
     int fr, min_inl, J, M;
+    float invJ;            // 1/J: scale index of a cell = floor((d + J - 1 + 0.5) * invJ)
     const int32_t *x, *y, *p;
     const uint32_t *t;
     const uint32_t *pix;   // x*H + y per event
     const uint32_t *skey;  // pixel ids, sorted
     const int32_t *P;      // event ids sorted by (pixel, id)
     const int32_t *pos;    // inverse of P
+    const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
     const int32_t *prev, *next;
-    int64_t *touch;        // (chunk seq << 32) | position of the first in-chunk event
-    int32_t *touch_last;   // position of the last in-chunk event
-    int64_t *sae;          // SAE snapshot: -1 never visited, else t
+    SaeCell *cells;        // SAE snapshot + in-chunk first event, per cell
+    int2 *tpos;            // positions in P of the first / last in-chunk event
     FlowCell *fsnap;       // flow snapshot
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
     uint8_t *valid;
-    uint64_t *bitmap;
+    uint64_t *bitmap;      // pooling candidates of the current chunk
+    uint32_t *wcount;      // popcount per bitmap word
+    uint32_t *woff;        // exclusive prefix of wcount (nwords + 1)
+    CandHdr *chdr;         // compacted candidates, ascending cell index
+    CandVal *cval;
+    int64_t nwords;
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // outputs
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
     int32_t *scale;
     int32_t *ox, *oy, *ot, *op;
-    unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells
+    unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells [3] cand [4] contrib
+    int2 *dbg_tc;                  // profiling only: per event (candidates scanned, contributors)
+    int32_t *defer;                // events whose fit needs the generic path
+    int *defer_count;
 };
 
 // ---------------------------------------------------------------------------
-// as-of lookup: position in P of the last event at pixel q with id <= e inside
-// the current chunk, or -1 when the snapshot (state before the chunk) applies.
-__device__ __forceinline__ int asof_pos(const Ctx &c, uint32_t q, int e, uint32_t seq) {
-    const int64_t tw = c.touch[q];
-    if ((uint32_t)((uint64_t)tw >> 32) != seq) return -1;
-    const int k = (int)(uint32_t)tw;
-    if (c.P[k] > e) return -1;
-    int hi = c.touch_last[q];
-    if (hi <= k) return k;
+// as-of lookups.  Position in P of the last event at pixel q with id <= e,
+// searched over the pixel's in-chunk run [tpos.x, tpos.y] (rare path: the
+// pixel fired more than once in the chunk and e is past its first event).
+__device__ __forceinline__ int run_search(const Ctx &c, uint32_t q, int e) {
+    const int2 tp = c.tpos[q];
+    int lo = tp.x, hi = tp.y;  // P[lo] <= e
     if (c.P[hi] <= e) return hi;
-    int lo = k;  // P[lo] <= e < P[hi], P ascending over the run
-    while (hi - lo > 1) {
+    while (hi - lo > 1) {  // P[lo] <= e < P[hi], P ascending over the run
         const int mid = (lo + hi) >> 1;
         if (c.P[mid] <= e) lo = mid;
         else hi = mid;
@@ -118,32 +161,48 @@ __device__ __forceinline__ int asof_pos(const Ctx &c, uint32_t q, int e, uint32_
     return lo;
 }
 
-// SAE stamp of pixel q as of event e: -1 never visited, else t.
-__device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
-    const int k = asof_pos(c, q, e, seq);
-    if (k >= 0) return (int64_t)c.t[c.P[k]];
-    return c.sae[q];
+// SAE stamp of pixel q as of event e (chunk seq) from its loaded cell:
+// -1 never visited, else t; -2 when the pixel fired 3+ times in the chunk and e
+// is past its second event (FAST) — the caller then takes the generic path.
+template <bool FAST>
+__device__ __forceinline__ int64_t sae_resolve(const Ctx &c, const SaeCell &s, uint32_t q, int e, uint32_t seq) {
+    if ((s.tag & kSeqMask) == seq) {
+        const int e1 = (int)(s.e1m & kSeqMask);
+        if (e1 <= e) {
+            if (!(s.e1m >> 31)) return (int64_t)s.t1;
+            const int e2 = (int)(s.e2m & kSeqMask);
+            if (e2 > e) return (int64_t)s.t1;
+            if (!(s.e2m >> 31)) return (int64_t)s.t2;
+            if (FAST) return -2;
+            return (int64_t)c.t[c.P[run_search(c, q, e)]];
+        }
+    }
+    return (s.tag >> 31) ? (int64_t)s.tsnap : int64_t(-1);
 }
 
-__device__ __forceinline__ FlowCell flow_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
-    const int k = asof_pos(c, q, e, seq);
-    if (k >= 0) return c.evf[c.P[k]];
-    return c.fsnap[q];
+__device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
+    return sae_resolve<false>(c, c.cells[q], q, e, seq);
 }
 
 // ---------------------------------------------------------------------------
 // prep
 
-__global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, int *err) {
+// Validate, pixel id, and the work-order key: (pooling chunk, 8x8 tile) so
+// that the threads of a wave and the waves of a CU work on neighbouring pixels.
+__global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int *err, int pool_chunk,
+                       int tile_bits) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= c.n) return;
     const int x = c.x[e], y = c.y[e];
+    uint32_t tile = 0;
     if (x < 0 || x >= c.W || y < 0 || y >= c.H) {
         atomicOr(err, 1);
         pix[e] = 0;
     } else {
         pix[e] = (uint32_t)x * (uint32_t)c.H + (uint32_t)y;
+        tile = (uint32_t)(x >> 3) * (uint32_t)((c.H + 7) >> 3) + (uint32_t)(y >> 3);
     }
+    wkey[e] = ((uint32_t)(e / pool_chunk) << tile_bits) | tile;
     iota[e] = e;
 }
 
@@ -185,21 +244,40 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
     }
 }
 
-// first / last in-chunk event of every pixel touched by chunk [c0, c1)
+// Record, for every pixel touched by chunk [c0, c1), its first in-chunk event
+// (inline in the SAE cell) and the bounds of its in-chunk run in P.
 __global__ void k_touch(Ctx c, int c0, int c1, uint32_t seq) {
     const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= c1) return;
     const uint32_t q = c.pix[e];
-    if (c.prev[e] < c0) c.touch[q] = (int64_t)(((uint64_t)seq << 32) | (uint32_t)c.pos[e]);
-    if (c.next[e] >= c1) c.touch_last[q] = c.pos[e];
+    const int nx = c.next[e];
+    if (c.prev[e] < c0) {  // first event of the pixel in the chunk
+        SaeCell *cell = &c.cells[q];
+        cell->tag = (cell->tag & ~kSeqMask) | seq;
+        cell->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
+        cell->t1 = c.t[e];
+        c.tpos[q].x = c.pos[e];
+        if (nx < c1) {  // and the second one
+            const int nn = c.next[nx];
+            cell->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
+            cell->t2 = c.t[nx];
+        }
+    }
+    if (nx >= c1) c.tpos[q].y = c.pos[e];
 }
 
+// SAE snapshot <- last event of the chunk at each touched pixel.
 __global__ void k_sae_update(Ctx c, int c0, int c1) {
     const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= c1) return;
-    if (c.next[e] >= c1) c.sae[c.pix[e]] = (int64_t)c.t[e];
+    if (c.next[e] >= c1) {
+        SaeCell *cell = &c.cells[c.pix[e]];
+        cell->tag |= 0x80000000u;
+        cell->tsnap = c.t[e];
+    }
 }
 
+// Flow snapshot <- last event of the chunk at each touched pixel.
 __global__ void k_flow_update(Ctx c, int c0, int c1) {
     const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= c1) return;
@@ -250,18 +328,21 @@ __device__ __forceinline__ double det3_partialpivlu(const double a[9]) {
 }
 
 // ---------------------------------------------------------------------------
-// Local plane fit, one thread per event.  FR > 0: fRad known at compile time
-// (stamps of the chosen window kept in registers); FR == 0: any fRad.
+// Local plane fit of one event (computeLocalFlow + computeGrads).  FR > 0:
+// fRad known at compile time, fully unrolled, cell stamps kept in registers;
+// returns false (nothing written) if some pixel fired 3+ times in the chunk
+// and needs its run searched — the generic FR == 0 instance then redoes the
+// event out of line.  FR == 0: any fRad, every lookup complete.
 template <int FR>
-__global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq) {
-    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= c1) return;
+__device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, double &vx_out, double &vy_out) {
+    constexpr bool FAST = FR > 0;
     const int fr = FR > 0 ? FR : c.fr;
     const int side = 2 * fr + 1;
     const int np = side * side;
     const int W = c.W, H = c.H;
     const int ex = c.x[e], ey = c.y[e];
     const uint32_t te = c.t[e];
+    double vx = 0.0, vy = 0.0;
 
     // ---- window scores (vFlow.cpp:870-912): sum over the window of
     // (t_e - t_k) + 2^32 [t_k > t_e], exact as int64; ties: first strict min.
@@ -275,13 +356,23 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
         score[w] = 0;
         any |= wok[w];
     }
-    double vx = 0.0, vy = 0.0;
-    if (any) {
+    if (!any) { vx_out = 0.0; vy_out = 0.0; return true; }
+    bool slow = false;
+    if (FR > 0) {
+        // union of the 9 windows, one column (fixed du) at a time: the column's
+        // cells are loaded together, then resolved
+        constexpr int US = FR > 0 ? 4 * FR + 1 : 1;
 #pragma unroll
         for (int du = -2 * FR; du <= 2 * FR; ++du) {
-            if (FR == 0) break;
             const int u = ex + du;
             if (u < 0 || u >= W) continue;
+            SaeCell col[US];
+            const int cbase = u * H + ey;
+#pragma unroll
+            for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
+                const int v = ey + dv;
+                if (v >= 0 && v < H) col[dv + 2 * FR] = c.cells[cbase + dv];
+            }
 #pragma unroll
             for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
                 const int v = ey + dv;
@@ -293,7 +384,8 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
                     if (du - ou <= FR && ou - du <= FR && dv - ov <= FR && ov - dv <= FR && wok[w]) mask |= 1 << w;
                 }
                 if (!mask) continue;
-                const int64_t st = sae_asof(c, (uint32_t)u * (uint32_t)H + (uint32_t)v, e, seq);
+                const int64_t st = sae_resolve<FAST>(c, col[dv + 2 * FR], (uint32_t)(cbase + dv), e, seq);
+                slow |= st == -2;
                 const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
                 const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
 #pragma unroll
@@ -301,130 +393,152 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
                     if (mask & (1 << w)) score[w] += d;
             }
         }
-        if (FR == 0) {
-            for (int du = -2 * fr; du <= 2 * fr; ++du) {
-                const int u = ex + du;
-                if (u < 0 || u >= W) continue;
-                for (int dv = -2 * fr; dv <= 2 * fr; ++dv) {
-                    const int v = ey + dv;
-                    if (v < 0 || v >= H) continue;
-                    int mask = 0;
+        if (slow) return false;
+    } else {
+        for (int du = -2 * fr; du <= 2 * fr; ++du) {
+            const int u = ex + du;
+            if (u < 0 || u >= W) continue;
+            for (int dv = -2 * fr; dv <= 2 * fr; ++dv) {
+                const int v = ey + dv;
+                if (v < 0 || v >= H) continue;
+                int mask = 0;
 #pragma unroll
-                    for (int w = 0; w < 9; ++w) {
-                        const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
-                        if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
-                    }
-                    if (!mask) continue;
-                    const int64_t st = sae_asof(c, (uint32_t)u * (uint32_t)H + (uint32_t)v, e, seq);
-                    const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-                    const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
-#pragma unroll
-                    for (int w = 0; w < 9; ++w)
-                        if (mask & (1 << w)) score[w] += d;
+                for (int w = 0; w < 9; ++w) {
+                    const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
+                    if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
                 }
+                if (!mask) continue;
+                const int64_t st = sae_asof(c, (uint32_t)(u * H + v), e, seq);
+                const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+                const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+                for (int w = 0; w < 9; ++w)
+                    if (mask & (1 << w)) score[w] += d;
             }
-        }
-        // bestscore starts at MAXSTAMP + 1; sums compare exactly
-        const int64_t nn = np;
-        int64_t best = nn * ((int64_t(1) << 32) + 1);
-        int bw = -1;
-#pragma unroll
-        for (int w = 0; w < 9; ++w)
-            if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
-        if (bw >= 0 && !(best > nn * (int64_t(1) << 32))) {
-            // ---- gather the winning window, cx-major (vFlow.cpp:923-930)
-            const int bi = ex + (bw / 3 - 1) * fr, bj = ey + (bw % 3 - 1) * fr;
-            constexpr int NPC = FR > 0 ? (2 * FR + 1) * (2 * FR + 1) : 1;
-            uint32_t tks[NPC];
-            uint64_t vis = 0;
-            int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
-            auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
-                const int cx = bi + k / side - fr, cy = bj + k % side - fr;
-                if (FR > 0) {
-                    const bool vk = (vis >> k) & 1;
-                    X = vk ? cx : 0; Y = vk ? cy : 0; T = tks[k < NPC ? k : 0];
-                } else {
-                    const int64_t st = sae_asof(c, (uint32_t)cx * (uint32_t)H + (uint32_t)cy, e, seq);
-                    X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
-                }
-            };
-            if (FR > 0) {
-#pragma unroll
-                for (int k = 0; k < NPC; ++k) {
-                    const int cx = bi + k / (2 * FR + 1) - FR, cy = bj + k % (2 * FR + 1) - FR;
-                    const int64_t st = sae_asof(c, (uint32_t)cx * (uint32_t)H + (uint32_t)cy, e, seq);
-                    tks[k] = st >= 0 ? (uint32_t)st : 0u;
-                    if (st >= 0) vis |= uint64_t(1) << k;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < np; ++k) {
-                int64_t X, Y; uint32_t T;
-                cell(k, X, Y, T);
-                sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
-            }
-            // AtA, column-major (vFlow.cpp:1311)
-            const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
-                                 (double)sy,  (double)sx,  (double)sy, (double)np};
-            double DET = det3_partialpivlu(a);
-            int inliers = 0;
-            double dtdx = 0.0, dtdy = 0.0;
-            if (!(DET < 1)) {
-                DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
-                const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
-                const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
-                const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
-                const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
-                const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
-                const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
-                const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
-                const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
-                const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
-                // temp = (A2*At)*Y in Eigen's order
-                const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
-                const double cz = (double)te * kTsToSec;
-                double r0 = 0.0, r1 = 0.0, r2 = 0.0;
-#pragma unroll
-                for (int k = 0; k < np; ++k) {
-                    int64_t Xi, Yi; uint32_t T;
-                    cell(k, Xi, Yi, T);
-                    const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
-                    const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-                    double m0, m1, m2;
-                    if (gemm) {
-                        m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
-                        m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
-                        m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
-                    } else {
-                        m0 = (d0 * X + d3 * Y) + d6 * 1.0;
-                        m1 = (d1 * X + d4 * Y) + d7 * 1.0;
-                        m2 = (d2 * X + d5 * Y) + d8 * 1.0;
-                    }
-                    if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
-                    else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
-                }
-                if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
-                // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
-                const double dtdp = sqrt(r0 * r0 + r1 * r1);
-                const double ccx = (double)ex, ccy = (double)ey;
-#pragma unroll
-                for (int k = 0; k < np; ++k) {
-                    int64_t Xi, Yi; uint32_t T;
-                    cell(k, Xi, Yi, T);
-                    const double Tk = (double)T;
-                    const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-                    const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
-                    const double actualdt = yt - cz;
-                    if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
-                }
-                const double speed = 1.0 / dtdp;
-                const double angle = atan2(r0, r1);
-                dtdx = speed * cos(angle);
-                dtdy = speed * sin(angle);
-            }
-            if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
         }
     }
+    // bestscore starts at MAXSTAMP + 1; sums compare exactly
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) { vx_out = 0.0; vy_out = 0.0; return true; }
+
+    // ---- gather the winning window, cx-major (vFlow.cpp:923-930)
+    const int bi = ex + (bw / 3 - 1) * fr, bj = ey + (bw % 3 - 1) * fr;
+    constexpr int NPC = FR > 0 ? (2 * FR + 1) * (2 * FR + 1) : 1;
+    uint32_t tks[NPC];
+    uint64_t vis = 0;
+    if (FR > 0) {  // a column at a time, loads first (all cells were resolved above)
+        constexpr int SD = 2 * FR + 1;
+#pragma unroll
+        for (int cxo = 0; cxo < SD; ++cxo) {
+            const int cb = (bi + cxo - FR) * H + (bj - FR);
+            SaeCell col[SD];
+#pragma unroll
+            for (int cyo = 0; cyo < SD; ++cyo) col[cyo] = c.cells[cb + cyo];
+#pragma unroll
+            for (int cyo = 0; cyo < SD; ++cyo) {
+                const int k = cxo * SD + cyo;
+                const int64_t st = sae_resolve<FAST>(c, col[cyo], (uint32_t)(cb + cyo), e, seq);
+                tks[k] = st < 0 ? 0u : (uint32_t)st;
+                if (st >= 0) vis |= uint64_t(1) << k;
+            }
+        }
+    }
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+        const int cx = bi + k / side - fr, cy = bj + k % side - fr;
+        if (FR > 0) {
+            // opaque copies: every pass re-derives X, Y, Yt from the packed
+            // stamps instead of keeping 3 x NP doubles live (register budget)
+            uint64_t vv = vis;
+            uint32_t tt = tks[k < NPC ? k : 0];
+            asm volatile("" : "+v"(tt), "+v"(vv));
+            const bool vk = (vv >> k) & 1;
+            X = vk ? cx : 0; Y = vk ? cy : 0; T = tt;
+        } else {
+            const int64_t st = sae_asof(c, (uint32_t)(cx * H + cy), e, seq);
+            X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
+        }
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
+#pragma unroll
+    for (int k = 0; k < np; ++k) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    // AtA, column-major (vFlow.cpp:1311)
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    int inliers = 0;
+    double dtdx = 0.0, dtdy = 0.0;
+    if (!(DET < 1)) {
+        DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+        const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+        const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+        const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+        const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+        const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+        const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+        const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+        const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+        const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+        // temp = (A2*At)*Y in Eigen's order
+        const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+        const double cz = (double)te * kTsToSec;
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < np; ++k) {
+            int64_t Xi, Yi; uint32_t T;
+            cell(k, Xi, Yi, T);
+            const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+            const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+            double m0, m1, m2;
+            if (gemm) {
+                m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+                m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+                m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+            } else {
+                m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+                m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+                m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+            }
+            if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+            else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+        }
+        if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+        // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+        const double dtdp = sqrt(r0 * r0 + r1 * r1);
+        const double ccx = (double)ex, ccy = (double)ey;
+#pragma unroll
+        for (int k = 0; k < np; ++k) {
+            int64_t Xi, Yi; uint32_t T;
+            cell(k, Xi, Yi, T);
+            const double Tk = (double)T;
+            const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+            const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+            const double actualdt = yt - cz;
+            if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+        }
+        const double speed = 1.0 / dtdp;
+        const double angle = atan2(r0, r1);
+        dtdx = speed * cos(angle);
+        dtdy = speed * sin(angle);
+    }
+    if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
+    vx_out = vx;
+    vy_out = vy;
+    return true;
+}
+
+// Validity gate, flow-surface value and record of one fitted event.
+__device__ __forceinline__ void fit_store(const Ctx &c, int e, double vx, double vy) {
+    const uint32_t te = c.t[e];
+    const int ex = c.x[e], ey = c.y[e];
     // ---- validity gate and flow-surface value (vFlow.cpp:315-357, 384-403)
     const bool ok = !isnan(fabs(vx)) && !isnan(fabs(vy)) && vx != 0 && vy != 0;
     FlowCell f;
@@ -450,16 +564,39 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
     if (c.ox) { c.ox[e] = ex; c.oy[e] = ey; c.ot[e] = (int32_t)te; c.op[e] = c.p[e]; }
 }
 
+// One thread per event of chunk [c0, c1).  Events that meet a pixel with 3+
+// in-chunk events are deferred to k_fit_generic through a small work list.
+template <int FR>
+__global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq) {
+    const int w = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= c1) return;
+    const int e = c.Q[w];  // chunk [c0, c1) occupies positions [c0, c1) of Q
+    double vx, vy;
+    if (fit_event<FR>(c, e, seq, vx, vy)) fit_store(c, e, vx, vy);
+    else c.defer[atomicAdd(c.defer_count, 1)] = e;
+}
+
+// The deferred events (any fRad, every lookup complete); grid sized for the
+// whole chunk, the list length is read on the device.
+__global__ __launch_bounds__(256) void k_fit_generic(Ctx c, uint32_t seq) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *c.defer_count) return;
+    const int e = c.defer[i];
+    double vx, vy;
+    fit_event<0>(c, e, seq, vx, vy);
+    fit_store(c, e, vx, vy);
+}
+
 // ---------------------------------------------------------------------------
 // Candidate-cell bitmap for pooling chunk [c0, c1): bit q set if q is touched in
 // the chunk, or its snapshot flow is valid and within the kill time of some
-// event of the chunk.  One wave ballot per 64 cells.
+// event of the chunk (a superset of every cell that can contribute to any event
+// of the chunk).  One wave ballot per 64 cells, popcount per word.
 __global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = false;
     if (q < c.WH) {
-        const int64_t tw = c.touch[q];
-        act = (uint32_t)((uint64_t)tw >> 32) == seq;
+        act = (c.cells[q].tag & kSeqMask) == seq;
         if (!act) {
             const int64_t ft = c.ftime[q];
             const int64_t lo = (int64_t)c.ctmin[chunk_idx] - (int64_t)kKillUs;
@@ -468,106 +605,318 @@ __global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq) {
         }
     }
     const uint64_t b = __ballot(act);
-    if ((threadIdx.x & 63) == 0) c.bitmap[q >> 6] = b;
+    if ((threadIdx.x & 63) == 0 && (q >> 6) < c.nwords) {
+        c.bitmap[q >> 6] = b;
+        c.wcount[q >> 6] = (uint32_t)__popcll(b);
+    }
 }
 
+// Exclusive prefix of the per-word popcounts (single workgroup of 1024).
+__global__ __launch_bounds__(1024) void k_scan(Ctx c) {
+    __shared__ uint32_t part[1024];
+    const int64_t nw = c.nwords;
+    const int tid = threadIdx.x;
+    const int64_t per = (nw + 1023) / 1024;
+    const int64_t b = tid * per, e = b + per < nw ? b + per : nw;
+    uint32_t sum = 0;
+    for (int64_t w = b; w < e; ++w) sum += c.wcount[w];
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = tid >= off ? part[tid - off] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = tid ? part[tid - 1] : 0u;
+    for (int64_t w = b; w < e; ++w) {
+        c.woff[w] = run;
+        run += c.wcount[w];
+    }
+    if (tid == 1023) c.woff[nw] = part[1023];
+}
+
+// Candidate index of the first candidate with cell index >= L.
+__device__ __forceinline__ uint32_t cand_index(const Ctx &c, int64_t L) {
+    const int64_t w = L >> 6;
+    const int r = (int)(L & 63);
+    uint32_t k = c.woff[w];
+    if (r) k += (uint32_t)__popcll(c.bitmap[w] & ((1ull << r) - 1));
+    return k;
+}
+
+// Materialise the candidate records of the chunk (thread per cell).
+__global__ void k_fill(Ctx c, uint32_t seq) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= c.WH) return;
+    const uint64_t bits = c.bitmap[q >> 6];
+    const int r = (int)(q & 63);
+    if (!((bits >> r) & 1)) return;
+    const uint32_t k = c.woff[q >> 6] + (uint32_t)__popcll(bits & ((1ull << r) - 1));
+    const SaeCell s = c.cells[q];
+    const FlowCell snap = c.fsnap[q];
+    CandHdr hd;
+    CandVal v;
+    hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
+    hd.t_snap = snap.t;
+    v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
+    if ((s.tag & kSeqMask) == seq) {
+        const int e1 = (int)(s.e1m & kSeqMask);
+        const FlowCell f1 = c.evf[e1];
+        hd.e1 = e1;
+        hd.lin |= (s.e1m & 0x80000000u ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
+        hd.t1 = f1.t;
+        v.L1 = f1.L; v.Lc1 = f1.Lc; v.Ls1 = f1.Ls;
+    } else {
+        hd.e1 = INT_MAX;
+        hd.t1 = 0;
+        v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
+    }
+    c.chdr[k] = hd;
+    c.cval[k] = v;
+}
+
+// Butterfly sums over the 64 lanes: quad xor-1, xor-2, row half-mirror and
+// row mirror by DPP, then xor-16 / xor-32 by permute.  Every lane ends with the
+// same value (each step adds a pair in both orders), so the result does not
+// depend on which lane reads it.
+template <int CTRL>
+__device__ __forceinline__ int dpp32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+    const int lo = dpp32<CTRL>(__double2loint(v)), hi = dpp32<CTRL>(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp64<0x141>(v);  // row_half_mirror
+    v += dpp64<0x140>(v);  // row_mirror
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }
 __device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += dpp32<0xB1>(v);
+    v += dpp32<0x4E>(v);
+    v += dpp32<0x141>(v);
+    v += dpp32<0x140>(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
     return v;
 }
 
 // Multiscale pooling (computeTrueFlow, vFlow.cpp:952-1210): one wavefront per
-// valid event; lane l walks window rows i = i_lo + l, i_lo + l + 64.  Window rows
-// span x-major linear indices [i*H + j_lo, i*H + j_hi] with j clipped to W-1 as
-// the reference does (vFlow.cpp:1000/1113), so for W > H a row runs into the
-// next column (aliasing kept); indices >= W*H do not contribute.
+// valid event.
+//   Window: rows i in [x-M, x+M] span x-major cell ranges [i*H + j_lo, i*H + j_hi]
+//   with j clipped to W-1 as the reference does (vFlow.cpp:1000/1113): for W > H
+//   a row runs into the next column (aliasing kept); indices >= W*H do not
+//   contribute.  Each row is a contiguous slice of the chunk's candidate list
+//   (bitmap popcount prefix); the slices are flattened.
+//   Phase A: lanes scan the flattened candidates 64 at a time (coalesced 16-B
+//   headers), resolve each cell's state as of e, and compact the contributors
+//   (valid flow, |dt| < 500 us) into LDS in ascending cell order (ballot).
+//   Phase B: lane l accumulates a contiguous share of the contributor list into
+//   every scale that contains the cell, then a fixed butterfly sums the lanes.
+// The summation order depends only on the contributor list, so results are
+// bitwise independent of chunking and streaming splits, and identical
+// contributor sets give identical scale sums (tie rule of vFlow.cpp:1161).
 template <int K>
 __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t seq) {
-    const int lane = threadIdx.x & 63;
-    const int e = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (e >= c1) return;
+    __shared__ int s_pre[4][130];       // per wave: prefix of candidate counts over rows
+    __shared__ int s_a[4][128];         // per wave: first candidate of each row
+    __shared__ uint2 s_con[4][kPoolCap];  // per wave: contributors {ref, kind | k0 << 8}
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (w >= c1) return;
+    const int e = c.Q[w];  // events of the chunk in tile order
     if (!c.valid[e]) return;
     const int ex = c.x[e], ey = c.y[e];
-    const double te = (double)c.t[e];
+    const uint32_t teu = c.t[e];
     const int W = c.W, H = c.H, M = c.M, J = c.J;
     const int64_t WH = c.WH;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    double sL[K], sX[K], sY[K];
-    int cnt[K];
+    const int nrows = i_hi - i_lo + 1;  // <= 2M+1
+    // ---- per-row candidate slices and their prefix
+    int carry = 0;
+    for (int r0 = 0; r0 < nrows; r0 += 64) {
+        const int r = r0 + lane;
+        int a = 0, cnt = 0;
+        if (r < nrows) {
+            const int base = (i_lo + r) * H;
+            const int l0 = base + j_lo;
+            int l1 = base + j_hi;
+            if (l1 > (int)WH - 1) l1 = (int)WH - 1;
+            if (l0 <= l1) {
+                a = (int)cand_index(c, l0);
+                cnt = (int)cand_index(c, l1 + 1) - a;
+            }
+            s_a[wv][r] = a;
+        }
+        int incl = cnt;  // inclusive wave scan
 #pragma unroll
-    for (int k = 0; k < K; ++k) { sL[k] = 0.0; sX[k] = 0.0; sY[k] = 0.0; cnt[k] = 0; }
-    for (int i = i_lo + lane; i <= i_hi; i += 64) {
-        const int64_t base = (int64_t)i * H;
-        const int64_t l0 = base + j_lo;
-        int64_t l1 = base + j_hi;
-        if (l1 > WH - 1) l1 = WH - 1;
-        if (l0 > l1) continue;
-        for (int64_t w = l0 >> 6; w <= (l1 >> 6); ++w) {
-            uint64_t bits = c.bitmap[w];
-            const int64_t wb = w << 6;
-            if (wb < l0) bits &= ~0ull << (l0 - wb);
-            if (wb + 63 > l1) bits &= ~0ull >> (63 - (l1 - wb));
-            while (bits) {
-                const int b = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                const int64_t lin = wb + b;
-                const FlowCell f = flow_asof(c, (uint32_t)lin, e, seq);
-                if (f.L > 0 && fabs(te - (double)f.t) < kKillUs) {  // vFlow.cpp:1002/1115
-                    const int j = (int)(lin - base);
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += v;
+        }
+        if (r < nrows) s_pre[wv][r + 1] = carry + incl;
+        carry += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) s_pre[wv][0] = 0;
+    // the LDS arrays are private to this wave: a wavefront-scope fence orders
+    // the writes above before the reads below
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int total = carry;
+
+    // ---- phase A: stage contributors with rank in [pass*cap, (pass+1)*cap) in
+    // LDS; returns the total number of contributors
+    auto collect = [&](int pass) -> int {
+        const int rank_lo = pass * kPoolCap, rank_hi = rank_lo + kPoolCap;
+        int ncon = 0;
+        int r = 0;  // row of the next candidate this lane will locate
+        auto locate = [&](int f, int &row, int &k) {
+            while (f >= s_pre[wv][r + 1]) ++r;
+            row = r;
+            k = s_a[wv][r] + (f - s_pre[wv][r]);
+        };
+        // software pipeline: the header of step s+1 is in flight while step s
+        // is resolved
+        int rc = 0, kc = 0;
+        CandHdr hc{};
+        if (lane < total) { locate(lane, rc, kc); hc = c.chdr[kc]; }
+        for (int f0 = 0; f0 < total; f0 += 64) {
+            const int f = f0 + lane, fn = f + 64;
+            int rn = 0, kn = 0;
+            CandHdr hn{};
+            if (fn < total) { locate(fn, rn, kn); hn = c.chdr[kn]; }
+            bool con = false;
+            uint32_t ref = 0, meta = 0;
+            if (f < total) {
+                uint32_t tq, kind;
+                bool ok;
+                if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; kind = 0; ref = (uint32_t)kc; }
+                else if (!(hc.lin & kCandMore)) { ok = (hc.lin & kCandOneOk) != 0; tq = hc.t1; kind = 1; ref = (uint32_t)kc; }
+                else {  // several events at the cell inside the chunk: search its run
+                    const int sev = c.P[run_search(c, hc.lin & kCandLinMask, e)];
+                    const FlowCell fe = c.evf[sev];
+                    ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)sev;
+                }
+                // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
+                const int64_t dt = (int64_t)teu - (int64_t)tq;
+                if (ok && (uint64_t)(dt + 499) < 999u) {
+                    const int i = i_lo + rc;
+                    const int j = (int)(hc.lin & kCandLinMask) - i * H;
                     const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
                     const int d = di > dj ? di : dj;
-                    const int k0 = (d + J - 1) / J;  // smallest scale containing the cell
+                    // smallest scale containing the cell: ceil(d / J)
+                    const int k0 = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);
+                    meta = kind | ((uint32_t)k0 << 8);
+                    con = true;
+                }
+            }
+            const uint64_t bal = __ballot(con);
+            if (con) {
+                const int rank = ncon + (int)__popcll(bal & ((1ull << lane) - 1));
+                if (rank >= rank_lo && rank < rank_hi) s_con[wv][rank - rank_lo] = make_uint2(ref, meta);
+            }
+            ncon += (int)__popcll(bal);
+            hc = hn; rc = rn; kc = kn;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        return ncon;
+    };
+    auto value_of = [&](uint2 en, double &L, double &Lc, double &Ls) {
+        const uint32_t kind = en.y & 0xFF;
+        if (kind == 0) { const CandVal &v = c.cval[en.x]; L = v.L_snap; Lc = v.Lc_snap; Ls = v.Ls_snap; }
+        else if (kind == 1) { const CandVal &v = c.cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
+        else { const FlowCell fe = c.evf[en.x]; L = fe.L; Lc = fe.Lc; Ls = fe.Ls; }
+    };
+    // ---- phase B1: mean length per scale; lane l takes a contiguous share of
+    // each staged batch
+    double sL[K];
+    int cntk[K];
 #pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        if (k >= k0) { sL[k] += f.L; sX[k] += f.Lc; sY[k] += f.Ls; cnt[k] += 1; }
+    for (int k = 0; k < K; ++k) { sL[k] = 0.0; cntk[k] = 0; }
+    int npass = 1, ncon_total = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+        if (pass) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        ncon_total = collect(pass);
+        npass = ncon_total > kPoolCap ? (ncon_total + kPoolCap - 1) / kPoolCap : 1;
+        const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
+        for (int b = nb * lane / 64; b < nb * (lane + 1) / 64; ++b) {
+            const uint2 en = s_con[wv][b];
+            const int k0 = (int)(en.y >> 8);
+            double L, Lc, Ls;
+            value_of(en, L, Lc, Ls);
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk)
+                if (kk >= k0) { sL[kk] += L; cntk[kk] += 1; }
+        }
+    }
+    // first strict max of the mean length over scales (vFlow.cpp:1023-1059);
+    // every lane holds the same butterfly sums, so every lane finds the same k*
+    double maxv = 0.0;
+    int mi = 0, cnt_mi = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double sk = wave_sum(sL[k]);
+        const int ck = wave_sum_i(cntk[k]);
+        const double mean = ck > 0 ? sk / (double)ck : 0.0;
+        if (mean > maxv) { maxv = mean; mi = k; cnt_mi = ck; }
+    }
+    // ---- phase B2: mean vector of the winning scale (vFlow.cpp:1067-1075)
+    double sX = 0.0, sY = 0.0;
+    if (maxv > 0) {
+        for (int pass = 0; pass < npass; ++pass) {
+            if (npass > 1) {  // re-stage batch `pass` (a single batch is still in LDS)
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                collect(pass);
+            }
+            const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
+            for (int b = nb * lane / 64; b < nb * (lane + 1) / 64; ++b) {
+                const uint2 en = s_con[wv][b];
+                if ((int)(en.y >> 8) <= mi) {
+                    double L, Lc, Ls;
+                    value_of(en, L, Lc, Ls);
+                    sX += Lc;
+                    sY += Ls;
                 }
             }
         }
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        sL[k] = wave_sum(sL[k]);
-        sX[k] = wave_sum(sX[k]);
-        sY[k] = wave_sum(sY[k]);
-        cnt[k] = wave_sum_i(cnt[k]);
-    }
+    sX = wave_sum(sX);
+    sY = wave_sum(sY);
     if (lane == 0) {
-        // per-scale means, first strict max of mean length (vFlow.cpp:1023-1075)
-        double maxv = 0.0, gx = 0.0, gy = 0.0;
-        int mi = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double mean = cnt[k] > 0 ? sL[k] / (double)cnt[k] : 0.0;
-            if (mean > maxv) { maxv = mean; mi = k; }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (k == mi) {
-                gx = cnt[k] > 0 ? sX[k] / (double)cnt[k] : 0.0;
-                gy = cnt[k] > 0 ? sY[k] / (double)cnt[k] : 0.0;
-            }
-        int sc = mi * J;
-        if (!(maxv > 0)) {  // vFlow.cpp:1085-1094
+        double gx, gy;
+        int sc;
+        if (maxv > 0) {
+            gx = sX / (double)cnt_mi;
+            gy = sY / (double)cnt_mi;
+            sc = mi * J;
+        } else {  // vFlow.cpp:1085-1094
             const FlowCell self = c.evf[e];
             gx = self.Lc; gy = self.Ls; sc = 0;
         }
         c.r_true[e] = sqrt(gy * gy + gx * gx);  // vFlow.cpp:365-366
         c.th_true[e] = atan2(gy, gx);
         c.scale[e] = sc;
+        if (c.dbg_tc) c.dbg_tc[e] = make_int2(total, ncon_total);
     }
 }
 
 // Algorithmic-work counters for the roofline: U_loc per event,
 // U_pool per valid event, valid count.  Grid-stride, one atomic per block.
 __global__ void k_stats(Ctx c) {
-    unsigned long long nv = 0, usae = 0, upool = 0;
+    unsigned long long nv = 0, usae = 0, upool = 0, ncand = 0, ncon = 0;
     const int fr = c.fr;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < c.n;
          e += (int64_t)gridDim.x * blockDim.x) {
@@ -577,6 +926,7 @@ __global__ void k_stats(Ctx c) {
         usae += (unsigned long long)(u1 - u0 + 1) * (unsigned long long)(v1 - v0 + 1);
         if (c.valid[e]) {
             ++nv;
+            if (c.dbg_tc) { const int2 tc = c.dbg_tc[e]; ncand += (unsigned)tc.x; ncon += (unsigned)tc.y; }
             const int i_lo = max(0, x - c.M), i_hi = min(c.W - 1, x + c.M);
             const int j_lo = max(0, y - c.M), j_hi = min(c.W - 1, y + c.M);
             for (int i = i_lo; i <= i_hi; ++i) {
@@ -587,16 +937,17 @@ __global__ void k_stats(Ctx c) {
             }
         }
     }
-    __shared__ unsigned long long s[3][256];
+    __shared__ unsigned long long s[5][256];
     s[0][threadIdx.x] = nv; s[1][threadIdx.x] = usae; s[2][threadIdx.x] = upool;
+    s[3][threadIdx.x] = ncand; s[4][threadIdx.x] = ncon;
     __syncthreads();
     for (int st = blockDim.x / 2; st > 0; st >>= 1) {
         if ((int)threadIdx.x < st)
-            for (int r = 0; r < 3; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
+            for (int r = 0; r < 5; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
         __syncthreads();
     }
     if (threadIdx.x == 0)
-        for (int r = 0; r < 3; ++r) atomicAdd(&c.counters[r], s[r][0]);
+        for (int r = 0; r < 5; ++r) atomicAdd(&c.counters[r], s[r][0]);
 }
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
@@ -612,11 +963,16 @@ struct farms_handle {
     int64_t WH = 0;
     int fit_chunk = kDefaultFitChunk, pool_chunk = kDefaultPoolChunk;
     hipStream_t stream = nullptr;
-    // persistent surfaces
-    int64_t *sae = nullptr, *ftime = nullptr, *touch = nullptr;
+    // persistent surfaces (x-major, W*H cells)
+    SaeCell *cells = nullptr;
+    int2 *tpos = nullptr;
+    int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    int32_t *touch_last = nullptr;
+    // per pooling chunk
     uint64_t *bitmap = nullptr;
+    uint32_t *wcount = nullptr, *woff = nullptr;
+    CandHdr *chdr = nullptr;
+    CandVal *cval = nullptr;
     int64_t nwords = 0;
     uint32_t seq = 0;
     // per-call workspace
@@ -624,14 +980,19 @@ struct farms_handle {
     int32_t *x = nullptr, *y = nullptr, *p = nullptr;
     uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
     int32_t *iota = nullptr, *P = nullptr, *pos = nullptr, *prev = nullptr, *next = nullptr;
+    int32_t *Q = nullptr;
+    uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
+    int tile_bits = 0;
     uint8_t *valid = nullptr;
     FlowCell *evf = nullptr;
+    int2 *dbg_tc = nullptr;
     double *o_d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     int32_t *o_scale = nullptr;
     uint32_t *ctmin = nullptr, *ctmax = nullptr;
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
-    int *err = nullptr;
+    int *err = nullptr, *defer_count = nullptr;
+    int32_t *defer = nullptr;
     unsigned long long *counters = nullptr;
     bool profiling = false;
     hipEvent_t ev[8] = {};
@@ -656,7 +1017,8 @@ void dfree(T *&p) {
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->pos); dfree(h->prev); dfree(h->next);
-    dfree(h->valid); dfree(h->evf); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
+    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
+    dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->defer); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
     h->cub_bytes = 0;
@@ -678,17 +1040,22 @@ int ensure_capacity(farms_handle *h, int64_t n) {
     if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
         (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
         (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->pos, cap)) ||
+        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
-        (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
+        (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
+        (rc = dalloc(&h->defer, std::min<int64_t>(cap, h->fit_chunk))) || (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
         (rc = dalloc(&h->ctmax, nch))) {
         free_workspace(h);
         return rc;
     }
     for (auto &d : h->o_d)
         if ((rc = dalloc(&d, cap))) { free_workspace(h); return rc; }
-    size_t bytes = 0;
+    size_t bytes = 0, bytes2 = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, h->pix, h->skey, h->iota, h->P, (int)cap, 0,
                                               end_bit_for(h->WH), h->stream));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, h->wkey, h->wkey_sorted, h->iota, h->Q, (int)cap, 0,
+                                              32, h->stream));
+    bytes = std::max(bytes, bytes2);
     if ((rc = dalloc((uint8_t **)&h->cub_tmp, bytes))) { free_workspace(h); return rc; }
     h->cub_bytes = bytes;
     h->cap = cap;
@@ -696,11 +1063,11 @@ int ensure_capacity(farms_handle *h, int64_t n) {
 }
 
 int reset_surfaces(farms_handle *h) {
-    HIPCHK(hipMemsetAsync(h->sae, 0xFF, sizeof(int64_t) * h->WH, h->stream));     // -1: never visited
+    // tag 0: never visited, never touched (chunk seqs start at 1)
+    HIPCHK(hipMemsetAsync(h->cells, 0, sizeof(SaeCell) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->tpos, 0, sizeof(int2) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->touch, 0, sizeof(int64_t) * h->WH, h->stream));      // seq 0 = never
-    HIPCHK(hipMemsetAsync(h->touch_last, 0, sizeof(int32_t) * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     return FARMS_OK;
@@ -752,15 +1119,21 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     Ctx c{};
     c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH;
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
+    c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.pos = h->pos; c.prev = h->prev; c.next = h->next;
-    c.touch = h->touch; c.touch_last = h->touch_last; c.sae = h->sae; c.fsnap = h->fsnap; c.ftime = h->ftime;
-    c.evf = h->evf; c.valid = h->valid; c.bitmap = h->bitmap; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
+    c.Q = h->Q;
+    c.cells = h->cells; c.tpos = h->tpos; c.fsnap = h->fsnap; c.ftime = h->ftime;
+    c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
+    c.bitmap = h->bitmap; c.wcount = h->wcount; c.woff = h->woff; c.chdr = h->chdr; c.cval = h->cval; c.nwords = h->nwords;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
     if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
     c.counters = h->counters;
+    c.dbg_tc = h->profiling ? h->dbg_tc : nullptr;
+    c.defer = h->defer;
+    c.defer_count = h->defer_count;
 
     const bool prof = h->profiling;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
@@ -771,7 +1144,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     }
     // ---- prep: validate, pixel ids, sort by pixel, links
     HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->err);
+    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->wkey, h->err,
+                       h->pool_chunk, h->tile_bits);
     int herr = 0;
     HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -780,6 +1154,15 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
                                               end_bit_for(h->WH), s));
     hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next);
+    {
+        const int nchunks = ceil_div(n, h->pool_chunk);
+        int cb = 1;
+        while ((1 << cb) < nchunks) ++cb;
+        if (cb + h->tile_bits > 32) return fail(FARMS_EINVAL, "too many pooling chunks for one call; raise pool_chunk");
+        size_t b2 = h->cub_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, b2, h->wkey, h->wkey_sorted, h->iota, h->Q, n, 0,
+                                                  h->tile_bits + cb, s));
+    }
     const int nch = ceil_div(n, h->pool_chunk);
     hipLaunchKernelGGL(k_chunk_minmax, dim3(nch), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
@@ -792,7 +1175,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         const dim3 g(ceil_div(c1 - c0, 256)), b(256);
         hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches], s));
+        HIPCHK(hipMemsetAsync(h->defer_count, 0, sizeof(int), s));
         launch_fit(c, h->fr, c0, c1, seq, s);
+        if (h->fr >= 1 && h->fr <= 3)
+            hipLaunchKernelGGL(k_fit_generic, g, b, 0, s, c, seq);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches + 1], s));
         hipLaunchKernelGGL(k_sae_update, g, b, 0, s, c, c0, c1);
         ++fit_launches;
@@ -804,12 +1190,15 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     pool_launcher pl = pool_for(h->K);
     int pool_launches = 0;
     const int bm_blocks = ceil_div(h->nwords * 64, 256);
+    const int cell_blocks = ceil_div(h->WH, 256);
     for (int ch = 0, c0 = 0; c0 < n; ++ch, c0 += h->pool_chunk) {
         const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->pool_chunk, n);
         const uint32_t seq = ++h->seq;
         const dim3 g(ceil_div(c1 - c0, 256)), b(256);
         hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
         hipLaunchKernelGGL(k_bitmap, dim3(bm_blocks), dim3(256), 0, s, c, ch, seq);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, c);
+        hipLaunchKernelGGL(k_fill, dim3(cell_blocks), dim3(256), 0, s, c, seq);
         const size_t ke = 2 * ((size_t)n_fit_chunks + pool_launches);
         if (prof) HIPCHK(hipEventRecord(h->kev[ke], s));
         pl(c, c0, c1, seq, s);
@@ -820,7 +1209,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     HIPCHK(hipGetLastError());
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (prof) {
-        HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 3, s));
+        HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 5, s));
         hipLaunchKernelGGL(k_stats, dim3(1024), dim3(256), 0, s, c);
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -850,11 +1239,13 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         st.ms_fit_kernel = kf;
         st.ms_pool_kernel = kp;
-        unsigned long long cnt[3];
+        unsigned long long cnt[5];
         HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
         st.n_valid = (int64_t)cnt[0];
         st.sae_cells = (double)cnt[1];
         st.pool_cells = (double)cnt[2];
+        st.pool_candidates = (double)cnt[3];
+        st.pool_contributors = (double)cnt[4];
     }
     h->stats = st;
     return FARMS_OK;
@@ -878,7 +1269,7 @@ extern "C" int farms_default_params(farms_params *o) {
 extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (!prm || !out) return fail(FARMS_EINVAL, "null argument");
     *out = nullptr;
-    if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height >= (int64_t(1) << 31))
+    if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height >= (int64_t(1) << 29))
         return fail(FARMS_EINVAL, "sensor size out of range");
     if (prm->window_jump <= 0 || prm->max_window < 0) return fail(FARMS_EINVAL, "bad pooling scales");
     const int K = prm->max_window / prm->window_jump + 1;
@@ -901,15 +1292,22 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
     h->nwords = (h->WH + 63) / 64;
+    // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
+    h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
+    {
+        const int64_t tiles = (int64_t)((h->W + 7) >> 3) * ((h->H + 7) >> 3);
+        while ((int64_t(1) << h->tile_bits) < tiles) ++h->tile_bits;
+    }
     int rc = FARMS_OK;
     auto bail = [&](int code) { farms_destroy(h); return code; };
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
-    if ((rc = dalloc(&h->sae, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) || (rc = dalloc(&h->touch, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->touch_last, h->WH)) ||
-        (rc = dalloc(&h->bitmap, h->nwords)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 4)))
+    if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->tpos, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->bitmap, h->nwords)) ||
+        (rc = dalloc(&h->wcount, h->nwords)) || (rc = dalloc(&h->woff, h->nwords + 1)) ||
+        (rc = dalloc(&h->chdr, h->WH)) || (rc = dalloc(&h->cval, h->WH)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->defer_count, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
@@ -920,8 +1318,8 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (!h) return FARMS_OK;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_workspace(h);
-    dfree(h->sae); dfree(h->ftime); dfree(h->touch); dfree(h->fsnap); dfree(h->touch_last);
-    dfree(h->bitmap); dfree(h->err); dfree(h->counters);
+    dfree(h->cells); dfree(h->tpos); dfree(h->ftime); dfree(h->fsnap);
+    dfree(h->bitmap); dfree(h->wcount); dfree(h->woff); dfree(h->chdr); dfree(h->cval); dfree(h->err); dfree(h->defer_count); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);

@@ -68,6 +68,8 @@ class FarmsStats(ctypes.Structure):
         ("ms_total", ctypes.c_double),
         ("ms_fit_kernel", ctypes.c_double),
         ("ms_pool_kernel", ctypes.c_double),
+        ("pool_candidates", ctypes.c_double),
+        ("pool_contributors", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--events", type=int, default=0, help="override the stream length")
     ap.add_argument("--fit-chunk", type=int, default=0)
     ap.add_argument("--pool-chunk", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=400_000, help="events in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -154,7 +154,9 @@ def main():
                    "ms_prep": round(st["ms_prep"], 3), "ms_fit_sweep": round(st["ms_fit"], 3),
                    "ms_pool_sweep": round(st["ms_pool"], 3), "ms_pool_kernel": round(pool_ms, 3),
                    "ms_fit_kernel": round(st["ms_fit_kernel"], 3),
-                   "dense_equiv_bytes_per_event": round(alg_bytes / max(n, 1), 1)},
+                   "dense_equiv_bytes_per_event": round(alg_bytes / max(n, 1), 1),
+                   "cand_per_valid": round(st["pool_candidates"] / max(st["n_valid"], 1), 1),
+                   "contrib_per_valid": round(st["pool_contributors"] / max(st["n_valid"], 1), 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ev, W, H, fs, jump, maxw, args.cpu_sample)

@@ -72,6 +72,8 @@ typedef struct {
     double ms_prep, ms_fit, ms_pool, ms_total;  /* phases: prep / fit sweep / pool sweep */
     double ms_fit_kernel;   /* sum of k_fit launch durations */
     double ms_pool_kernel;  /* sum of k_pool launch durations */
+    double pool_candidates;   /* sum over valid events of candidate cells scanned */
+    double pool_contributors; /* sum over valid events of contributing cells (largest scale) */
 } farms_stats;
 
 /* vFlowManager ctor defaults: 320 x 320, filter 3, 5 inliers (main.cpp:21-24),

@@ -913,6 +913,15 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
     }
 }
 
+// lastEventTime surface for farms_get_last_event_time: stamp of the latest
+// event at each pixel, 0 when never visited (vFlow.cpp:66,264,407).
+__global__ void k_last_time(const SaeCell *cells, int64_t WH, double *out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= WH) return;
+    const SaeCell s = cells[q];
+    out[q] = (s.tag >> 31) ? (double)s.tsnap : 0.0;
+}
+
 // Algorithmic-work counters for the roofline: U_loc per event,
 // U_pool per valid event, valid count.  Grid-stride, one atomic per block.
 __global__ void k_stats(Ctx c) {
@@ -1347,6 +1356,19 @@ extern "C" int farms_get_stats(const farms_handle *h, farms_stats *out) {
 }
 
 extern "C" int farms_num_scales(const farms_handle *h) { return h ? h->K : 0; }
+
+extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
+    if (!h || !out) return fail(FARMS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(h->prm.device));
+    double *d = nullptr;
+    HIPCHK(hipMalloc((void **)&d, sizeof(double) * h->WH));
+    hipLaunchKernelGGL(k_last_time, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, h->cells, h->WH, d);
+    hipError_t err = hipMemcpyAsync(out, d, sizeof(double) * h->WH, hipMemcpyDeviceToHost, h->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
+    (void)hipFree(d);
+    if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
+    return FARMS_OK;
+}
 
 extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
                                     const uint32_t *d_t, const int32_t *d_p, int64_t n, farms_records *d_out) {

@@ -100,7 +100,7 @@ class SynthParams(ctypes.Structure):
 HIP_SYMBOLS = (
     "farms_default_params", "farms_create", "farms_destroy", "farms_reset", "farms_process",
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
-    "farms_last_error",
+    "farms_get_last_event_time", "farms_last_error",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text")
 

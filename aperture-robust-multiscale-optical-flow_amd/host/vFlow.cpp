@@ -1,0 +1,131 @@
+// vFlow.cpp — host-side vFlowManager (see vFlow.h).
+//
+// runFileCopy follows /root/reference/src/vFlow.cpp:111-460 step for step:
+// same console lines, same file names, same parse semantics (event_io), same
+// timed region (after the parse, before the write), same 11 output columns.
+// The per-event loop (vFlow.cpp:223-414) is one farms_process call.
+#include "vFlow.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <iostream>
+#include <stdexcept>
+
+#include "event_io.h"
+
+vFlowManager::vFlowManager(int height, int width, int filterSize, int minEvtsOnPlane)
+    : vFlowManager(height, width, filterSize, minEvtsOnPlane, std::string()) {}
+
+vFlowManager::vFlowManager(int height, int width, int filterSize, int minEvtsOnPlane, std::string fileName) {
+    std::cout << "[debug] : Begin creating vFlowManager object" << std::endl;  // vFlow.cpp:26
+    farms_default_params(&prm);
+    prm.height = height;
+    prm.width = width;
+    prm.filter_size = filterSize;  // normalised by the library as vFlow.cpp:32-36
+    prm.min_inliers = minEvtsOnPlane;
+    fileNameInput = fileName;
+}
+
+vFlowManager::~vFlowManager() { close(); }
+
+void vFlowManager::close() {
+    if (handle) farms_destroy(handle);
+    handle = nullptr;
+}
+
+void vFlowManager::setScales(int windowJump, int maxWindow) {
+    prm.window_jump = windowJump;
+    prm.max_window = maxWindow;
+    close();
+}
+
+void vFlowManager::setDevice(int device) {
+    prm.device = device;
+    close();
+}
+
+int vFlowManager::ensure_handle() {
+    if (handle) return FARMS_OK;
+    return farms_create(&prm, &handle);
+}
+
+EventMatrix<double> vFlowManager::returnFlowTime() {
+    EventMatrix<double> m(prm.width, prm.height, 0.0);
+    if (handle) farms_get_last_event_time(handle, m.data());
+    return m;
+}
+
+// The timed per-event loop over the parsed X/Y/T/POL (vFlow.cpp:194-423).
+long vFlowManager::process(bool write_output) {
+    const int64_t n = (int64_t)T.size();
+    if (n == 0) {
+        // the reference dies here with std::out_of_range from T.at(0) (vFlow.cpp:194)
+        throw std::out_of_range("no events read from " + fileNameInput);
+    }
+    const unsigned int t0 = T.at(0);
+    std::cout << "First time = " << t0 << std::endl;
+    std::cout << "Processing events " << std::endl;
+    int rc = ensure_handle();
+    if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_create: ") + farms_last_error());
+
+    std::vector<uint32_t> t_rel((size_t)n);
+    std::vector<int32_t> p((size_t)n);
+    std::vector<int32_t> ox((size_t)n), oy((size_t)n), ot((size_t)n), op((size_t)n), osc((size_t)n);
+    std::vector<double> rt((size_t)n), tt((size_t)n), vx((size_t)n), vy((size_t)n), rl((size_t)n), tl((size_t)n);
+    farms_records rec{ox.data(), oy.data(), ot.data(), op.data(), rt.data(), tt.data(),
+                      vx.data(), vy.data(), rl.data(), tl.data(), osc.data()};
+
+    const auto start = std::chrono::system_clock::now();  // vFlow.cpp:214
+    for (int64_t e = 0; e < n; ++e) {
+        t_rel[(size_t)e] = T[(size_t)e] - t0;                   // vFlow.cpp:240-241
+        p[(size_t)e] = POL[(size_t)e] < 0 ? 0 : POL[(size_t)e];  // vFlow.cpp:245-247
+    }
+    rc = farms_process(handle, X.data(), Y.data(), t_rel.data(), p.data(), n, &rec);
+    const auto stop = std::chrono::system_clock::now();  // vFlow.cpp:416
+    if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_process: ") + farms_last_error());
+    numEvents += (double)n;
+    const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(stop - start).count();
+
+    std::cout << std::endl << "Done processing!" << std::endl;
+    if (write_output) {
+        std::cout << std::endl << "Writing output file." << std::endl;
+        const std::string out = fileNameInput + "_FARMSOut_batch.txt";  // vFlow.cpp:131
+        if (!farms_io::write_records(out, rec, n)) std::cerr << "cannot write " << out << std::endl;
+    }
+    return us;
+}
+
+long vFlowManager::runFileCopy(unsigned long int NUMEVENTS) {
+    const std::string in = fileNameInput + ".txt";  // vFlow.cpp:150
+    std::cout << in << std::endl;
+    std::cout << "Reading input file " << std::endl;
+    farms_io::EventColumns cols;
+    int64_t nread = 0;
+    farms_io::read_events(in, NUMEVENTS, cols, nread);  // an unopenable file reads 0 events
+    X.insert(X.end(), cols.X.begin(), cols.X.end());
+    Y.insert(Y.end(), cols.Y.begin(), cols.Y.end());
+    T.insert(T.end(), cols.T.begin(), cols.T.end());
+    POL.insert(POL.end(), cols.POL.begin(), cols.POL.end());
+    std::cout << "Done reading " << nread << " Events." << std::endl;
+    return process(true);
+}
+
+// Serial mode (vFlow.cpp:465-826) is the reference's streaming variant: it
+// writes no output file and reports the summed per-event compute time.  Here it
+// runs the same accelerated loop and reports its time; its per-event semantics
+// (first event skipped, lastEventTime written after pooling) are not
+// reproduced — see DESIGN.md §7.
+long vFlowManager::run(unsigned long int NUMEVENTS) {
+    const std::string in = fileNameInput + ".txt";
+    std::cout << in << std::endl;
+    farms_io::EventColumns cols;
+    int64_t nread = 0;
+    if (!farms_io::read_events(in, NUMEVENTS, cols, nread)) {
+        std::cout << "Unable to open file" << std::endl;  // vFlow.cpp:802
+        return 0;
+    }
+    X = cols.X; Y = cols.Y; T = cols.T; POL = cols.POL;
+    const long us = process(false);
+    std::cout << std::endl << "Done!" << std::endl;
+    return us;
+}

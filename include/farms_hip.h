@@ -104,6 +104,11 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
 int farms_set_profiling(farms_handle *h, int enable);
 int farms_get_stats(const farms_handle *h, farms_stats *out);
 
+/* Copy the lastEventTime surface (vFlow.h:73, x-major W x H doubles: the stamp
+ * of the latest event at each pixel, 0 if none) into host memory; the
+ * reference exposes it as returnFlowTime() (vFlow.h:107). */
+int farms_get_last_event_time(const farms_handle *h, double *out);
+
 /* Number of pooling scales, floor(max_window / window_jump) + 1. */
 int farms_num_scales(const farms_handle *h);
 

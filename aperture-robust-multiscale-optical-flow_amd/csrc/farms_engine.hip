@@ -111,7 +111,10 @@ constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
 
 struct Ctx {
     int W, H, n;
-    int64_t WH;
+    int64_t WH;            // cells stored by this handle (region columns x H)
+    int64_t WHs;           // cells of the whole sensor (W x H): the pooling window's end
+    int X0, XR1;           // stored region: columns [X0, XR1); cell index = (x - X0) * H + y
+    int own_lo, own_hi;    // pooled (owned) columns [own_lo, own_hi)
     int fr, min_inl, J, M;
     float invJ;            // 1/J: scale index of a cell = floor((d + J - 1 + 0.5) * invJ)
     const int32_t *x, *y, *p;
@@ -195,12 +198,12 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
     if (e >= c.n) return;
     const int x = c.x[e], y = c.y[e];
     uint32_t tile = 0;
-    if (x < 0 || x >= c.W || y < 0 || y >= c.H) {
+    if (x < c.X0 || x >= c.XR1 || y < 0 || y >= c.H) {
         atomicOr(err, 1);
         pix[e] = 0;
     } else {
-        pix[e] = (uint32_t)x * (uint32_t)c.H + (uint32_t)y;
-        tile = (uint32_t)(x >> 3) * (uint32_t)((c.H + 7) >> 3) + (uint32_t)(y >> 3);
+        pix[e] = (uint32_t)(x - c.X0) * (uint32_t)c.H + (uint32_t)y;
+        tile = (uint32_t)((x - c.X0) >> 3) * (uint32_t)((c.H + 7) >> 3) + (uint32_t)(y >> 3);
     }
     wkey[e] = ((uint32_t)(e / pool_chunk) << tile_bits) | tile;
     iota[e] = e;
@@ -366,12 +369,14 @@ __device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, dou
         for (int du = -2 * FR; du <= 2 * FR; ++du) {
             const int u = ex + du;
             if (u < 0 || u >= W) continue;
+            const bool inr = u >= c.X0 && u < c.XR1;  // outside the stored region: never visited
             SaeCell col[US];
-            const int cbase = u * H + ey;
+            const int cbase = (u - c.X0) * H + ey;
 #pragma unroll
             for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
                 const int v = ey + dv;
-                if (v >= 0 && v < H) col[dv + 2 * FR] = c.cells[cbase + dv];
+                col[dv + 2 * FR] = SaeCell{};
+                if (inr && v >= 0 && v < H) col[dv + 2 * FR] = c.cells[cbase + dv];
             }
 #pragma unroll
             for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
@@ -408,7 +413,8 @@ __device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, dou
                     if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
                 }
                 if (!mask) continue;
-                const int64_t st = sae_asof(c, (uint32_t)(u * H + v), e, seq);
+                const int64_t st = (u >= c.X0 && u < c.XR1) ? sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq)
+                                                            : int64_t(-1);
                 const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
                 const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
 #pragma unroll
@@ -435,10 +441,12 @@ __device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, dou
         constexpr int SD = 2 * FR + 1;
 #pragma unroll
         for (int cxo = 0; cxo < SD; ++cxo) {
-            const int cb = (bi + cxo - FR) * H + (bj - FR);
+            const int u = bi + cxo - FR;
+            const bool inr = u >= c.X0 && u < c.XR1;
+            const int cb = (u - c.X0) * H + (bj - FR);
             SaeCell col[SD];
 #pragma unroll
-            for (int cyo = 0; cyo < SD; ++cyo) col[cyo] = c.cells[cb + cyo];
+            for (int cyo = 0; cyo < SD; ++cyo) col[cyo] = inr ? c.cells[cb + cyo] : SaeCell{};
 #pragma unroll
             for (int cyo = 0; cyo < SD; ++cyo) {
                 const int k = cxo * SD + cyo;
@@ -459,7 +467,8 @@ __device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, dou
             const bool vk = (vv >> k) & 1;
             X = vk ? cx : 0; Y = vk ? cy : 0; T = tt;
         } else {
-            const int64_t st = sae_asof(c, (uint32_t)(cx * H + cy), e, seq);
+            const int64_t st = (cx >= c.X0 && cx < c.XR1) ? sae_asof(c, (uint32_t)((cx - c.X0) * H + cy), e, seq)
+                                                          : int64_t(-1);
             X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
         }
     };
@@ -734,9 +743,11 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
     const int e = c.Q[w];  // events of the chunk in tile order
     if (!c.valid[e]) return;
     const int ex = c.x[e], ey = c.y[e];
+    if (ex < c.own_lo || ex >= c.own_hi) return;  // halo event: fitted, pooled by its owner
     const uint32_t teu = c.t[e];
     const int W = c.W, H = c.H, M = c.M, J = c.J;
-    const int64_t WH = c.WH;
+    const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
+    const int WHs = (int)c.WHs;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     const int nrows = i_hi - i_lo + 1;  // <= 2M+1
@@ -747,9 +758,12 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
         int a = 0, cnt = 0;
         if (r < nrows) {
             const int base = (i_lo + r) * H;
-            const int l0 = base + j_lo;
             int l1 = base + j_hi;
-            if (l1 > (int)WH - 1) l1 = (int)WH - 1;
+            if (l1 > WHs - 1) l1 = WHs - 1;  // past the end of the sensor: no contribution
+            int l0 = base + j_lo - OFF;
+            l1 -= OFF;
+            if (l0 < 0) l0 = 0;               // outside the stored region: never visited
+            if (l1 > WHl - 1) l1 = WHl - 1;
             if (l0 <= l1) {
                 a = (int)cand_index(c, l0);
                 cnt = (int)cand_index(c, l1 + 1) - a;
@@ -809,7 +823,7 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
                 const int64_t dt = (int64_t)teu - (int64_t)tq;
                 if (ok && (uint64_t)(dt + 499) < 999u) {
                     const int i = i_lo + rc;
-                    const int j = (int)(hc.lin & kCandLinMask) - i * H;
+                    const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
                     const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
                     const int d = di > dj ? di : dj;
                     // smallest scale containing the cell: ceil(d / J)
@@ -933,7 +947,7 @@ __global__ void k_stats(Ctx c) {
         const int u0 = max(0, x - 2 * fr), u1 = min(c.W - 1, x + 2 * fr);
         const int v0 = max(0, y - 2 * fr), v1 = min(c.H - 1, y + 2 * fr);
         usae += (unsigned long long)(u1 - u0 + 1) * (unsigned long long)(v1 - v0 + 1);
-        if (c.valid[e]) {
+        if (c.valid[e] && x >= c.own_lo && x < c.own_hi) {
             ++nv;
             if (c.dbg_tc) { const int2 tc = c.dbg_tc[e]; ncand += (unsigned)tc.x; ncon += (unsigned)tc.y; }
             const int i_lo = max(0, x - c.M), i_hi = min(c.W - 1, x + c.M);
@@ -941,7 +955,7 @@ __global__ void k_stats(Ctx c) {
             for (int i = i_lo; i <= i_hi; ++i) {
                 const int64_t l0 = (int64_t)i * c.H + j_lo;
                 int64_t l1 = (int64_t)i * c.H + j_hi;
-                if (l1 > c.WH - 1) l1 = c.WH - 1;
+                if (l1 > c.WHs - 1) l1 = c.WHs - 1;
                 if (l1 >= l0) upool += (unsigned long long)(l1 - l0 + 1);
             }
         }
@@ -969,7 +983,8 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 struct farms_handle {
     farms_params prm;
     int W = 0, H = 0, fr = 0, J = 0, M = 0, K = 0;
-    int64_t WH = 0;
+    int64_t WH = 0;  // stored cells (region)
+    int X0 = 0, WR = 0, own_lo = 0, own_hi = 0;
     int fit_chunk = kDefaultFitChunk, pool_chunk = kDefaultPoolChunk;
     hipStream_t stream = nullptr;
     // persistent surfaces (x-major, W*H cells)
@@ -1126,7 +1141,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const int n = (int)n64;
     hipStream_t s = h->stream;
     Ctx c{};
-    c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH;
+    c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH; c.WHs = (int64_t)h->W * h->H;
+    c.X0 = h->X0; c.XR1 = h->X0 + h->WR; c.own_lo = h->own_lo; c.own_hi = h->own_hi;
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
@@ -1281,6 +1297,10 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height >= (int64_t(1) << 29))
         return fail(FARMS_EINVAL, "sensor size out of range");
     if (prm->window_jump <= 0 || prm->max_window < 0) return fail(FARMS_EINVAL, "bad pooling scales");
+    if (prm->region_width < 0 || (prm->region_width > 0 && (prm->region_x0 < 0 || prm->region_x0 + prm->region_width > prm->width)))
+        return fail(FARMS_EINVAL, "stored region outside the sensor");
+    if (prm->own_x1 < 0 || (prm->own_x1 > 0 && (prm->own_x0 < 0 || prm->own_x0 >= prm->own_x1 || prm->own_x1 > prm->width)))
+        return fail(FARMS_EINVAL, "bad owned column range");
     const int K = prm->max_window / prm->window_jump + 1;
     // spatialPool has maxWindow slots and is indexed with .at() (vFlow.cpp:966,1025)
     if (K > prm->max_window) return fail(FARMS_EINVAL, "more pooling scales than maxWindow (reference throws)");
@@ -1296,7 +1316,12 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (fs < 5) fs = 3;
     if (!(fs % 2)) fs--;
     h->fr = fs / 2;
-    h->W = prm->width; h->H = prm->height; h->WH = (int64_t)prm->width * prm->height;
+    h->W = prm->width; h->H = prm->height;
+    h->X0 = prm->region_width > 0 ? prm->region_x0 : 0;
+    h->WR = prm->region_width > 0 ? prm->region_width : prm->width;
+    h->own_lo = prm->own_x1 > 0 ? prm->own_x0 : 0;
+    h->own_hi = prm->own_x1 > 0 ? prm->own_x1 : prm->width;
+    h->WH = (int64_t)h->WR * prm->height;
     h->J = prm->window_jump; h->M = prm->max_window; h->K = K;
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
@@ -1363,7 +1388,9 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     double *d = nullptr;
     HIPCHK(hipMalloc((void **)&d, sizeof(double) * h->WH));
     hipLaunchKernelGGL(k_last_time, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, h->cells, h->WH, d);
-    hipError_t err = hipMemcpyAsync(out, d, sizeof(double) * h->WH, hipMemcpyDeviceToHost, h->stream);
+    for (int64_t q = 0; q < (int64_t)h->W * h->H; ++q) out[q] = 0.0;  // columns outside the region
+    hipError_t err = hipMemcpyAsync(out + (int64_t)h->X0 * h->H, d, sizeof(double) * h->WH, hipMemcpyDeviceToHost,
+                                    h->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
     (void)hipFree(d);
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));

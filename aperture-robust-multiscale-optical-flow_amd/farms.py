@@ -47,6 +47,10 @@ class FarmsParams(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("fit_chunk", ctypes.c_int32),
         ("pool_chunk", ctypes.c_int32),
+        ("region_x0", ctypes.c_int32),
+        ("region_width", ctypes.c_int32),
+        ("own_x0", ctypes.c_int32),
+        ("own_x1", ctypes.c_int32),
     ]
 
 
@@ -261,7 +265,7 @@ class FlowManager:
 
     def __init__(self, height: int = 320, width: int = 320, filter_size: int = 3, min_evts_on_plane: int = 5,
                  window_jump: int = 5, max_window: int = 50, device: int = 0, fit_chunk: int = 0,
-                 pool_chunk: int = 0):
+                 pool_chunk: int = 0, region: tuple | None = None, owned: tuple | None = None):
         self._lib = load_hip_library()
         prm = FarmsParams()
         _check(self._lib, self._lib.farms_default_params(ctypes.byref(prm)))
@@ -269,6 +273,10 @@ class FlowManager:
         prm.filter_size, prm.min_inliers = int(filter_size), int(min_evts_on_plane)
         prm.window_jump, prm.max_window = int(window_jump), int(max_window)
         prm.device, prm.fit_chunk, prm.pool_chunk = int(device), int(fit_chunk), int(pool_chunk)
+        if region is not None:  # (x0, x1): stored columns
+            prm.region_x0, prm.region_width = int(region[0]), int(region[1]) - int(region[0])
+        if owned is not None:  # (x0, x1): pooled columns
+            prm.own_x0, prm.own_x1 = int(owned[0]), int(owned[1])
         self.params = prm
         h = ctypes.c_void_p()
         _check(self._lib, self._lib.farms_create(ctypes.byref(prm), ctypes.byref(h)))

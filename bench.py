@@ -7,8 +7,12 @@ events, filtersize 5, inlierCheck 5 (the north_star's headline configuration).
 A step = one full pass of the hot path (surfaces reset + every event through
 local fit and multiscale pooling) over the whole resident stream.
 
-Multi-GPU (torchrun, one process per GPU): spatial x-strips, weak scaling — see
-DESIGN.md §6.
+Multi-GPU (torchrun, one process per GPU): weak scaling — the stream holds N x
+the per-GPU event count on the same sensor; rank r owns the events of one
+x-strip (event-count quantiles) and its handle stores the strip widened by the
+pooling + fit halo, so its records are bitwise those of a one-GPU run.  No
+data-path collective (strips.py); value = owned events of all
+ranks / max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -27,6 +31,7 @@ sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 
 import farms  # noqa: E402
+import strips  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720), 4: (1280, 720), 5: (1280, 720)}
@@ -70,34 +75,43 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # FARMS_BENCH_DEVICE pins every rank to one device (rehearsal of N ranks on a
+    # one-GPU box, with FARMS_DIST_BACKEND=gloo); the driver uses neither.
+    device = int(os.environ.get("FARMS_BENCH_DEVICE", local_rank))
+    backend = os.environ.get("FARMS_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", device)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     cfg = args.config
     W, H = SENSOR[cfg]
     fs = FILTER[cfg]
     jump, maxw = (25, 50) if cfg == 5 else (5, 50)
-    sp = farms.synth_params(cfg, args.events or None)
-    if cfg in (4, 5):
-        sp.n_events = args.events or 50_000_000  # per-GPU share fixed (weak scaling)
-    # weak scaling: every rank owns a full-size stream of its own (independent seed)
-    sp.seed = int(sp.seed) + 0x1000 * rank
-    ev = farms.synth_generate(sp)
-    n = len(ev)
+    sp = farms.synth_params(cfg)
+    per_gpu = args.events or (int(sp.n_events) if cfg in (1, 2, 3) else 50_000_000)
+    sp.n_events = per_gpu * world  # weak scaling: fixed events per GPU
+    ev = farms.synth_generate(sp)  # same seed on every rank: the same stream
     x, y, t, p = ev.relative()
+    strip = strips.plan(x, W, world, fs, maxw)[rank]
+    if world > 1:
+        m = strips.region_mask(x, strip)
+        x, y, t, p = x[m], y[m], t[m], p[m]
+    n = len(x)
+    n_owned = int(strips.owned_mask(x, strip).sum())
     dx = torch.from_numpy(x).to(dev)
     dy = torch.from_numpy(y).to(dev)
     dt_ = torch.from_numpy(t.view(np.int32)).to(dev)
     dp = torch.from_numpy(p).to(dev)
     out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
            for c in farms.COLUMNS[4:]}
-    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=local_rank,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk)
+    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk,
+                           region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi))
     torch.cuda.synchronize()
 
     def step():
@@ -120,14 +134,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        nn = torch.tensor([n], device=dev, dtype=torch.float64)
+        nn = torch.tensor([n_owned], device=red_dev, dtype=torch.float64)
         dist.all_reduce(nn)
         total_events = float(nn.item())
     else:
-        total_events = float(n)
+        total_events = float(n_owned)
 
     ms_step = elapsed / args.steps * 1e3
     value = total_events * args.steps / elapsed / 1e6
@@ -146,9 +160,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"BASELINE config {cfg}: {W}x{H} synthetic moving-bars stream, "
-                               f"{n} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
-                   "events_per_gpu": n, "width": W, "height": H, "filtersize": fs,
-                   "parallelism": f"{world} independent stream(s)" if world > 1 else "1 GPU"},
+                               f"{per_gpu} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
+                   "events_per_gpu": per_gpu, "width": W, "height": H, "filtersize": fs,
+                   "parallelism": (f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, "
+                                   "no data-path collective") if world > 1 else "1 GPU"},
         "roofline": roofline,
         "detail": {"valid_frac": round(st["n_valid"] / max(st["n_events"], 1), 4),
                    "ms_prep": round(st["ms_prep"], 3), "ms_fit_sweep": round(st["ms_fit"], 3),
@@ -160,6 +175,9 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ev, W, H, fs, jump, maxw, args.cpu_sample)
+    if world > 1:
+        line["detail"]["rank0_stored_events"] = n
+        line["detail"]["rank0_owned_events"] = n_owned
     fm.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -46,6 +46,16 @@ typedef struct {
     int32_t device;       /* HIP device ordinal */
     int32_t fit_chunk;    /* events per local-fit chunk, 0 = default */
     int32_t pool_chunk;   /* events per pooling chunk, 0 = default */
+    /* spatial strips (multi-GPU): the handle stores columns [region_x0,
+     * region_x0 + region_width) of the width x height sensor and pools only the
+     * events of columns [own_x0, own_x1); events of the other stored columns are
+     * fitted (their flows feed the owned events' pooling) and their r_true /
+     * theta_true / scale are left 0.  region_width = 0: the whole sensor;
+     * own_x1 = 0: every column.  With region = owned columns widened by
+     * max_window + 1 + 2 * (filter_size / 2) on each side (clipped to the
+     * sensor), owned records are bitwise those of a whole-sensor run. */
+    int32_t region_x0, region_width;
+    int32_t own_x0, own_x1;
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA

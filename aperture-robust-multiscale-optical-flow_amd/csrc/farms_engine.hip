@@ -104,6 +104,15 @@ struct __attribute__((aligned(16))) CandHdr {
 struct CandVal {
     double L_snap, Lc_snap, Ls_snap;
     double L1, Lc1, Ls1;
+    int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
+};
+
+// Pooling-sweep touch record of a cell (kept apart from the SAE cells so the
+// pooling chain can run concurrently with the fit sweep): seq of the chunk that
+// last touched the cell, its first in-chunk event | bit31 = more than one.
+struct PoolTouch {
+    uint32_t seq;
+    uint32_t e1m;
 };
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
@@ -131,12 +140,16 @@ struct Ctx {
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
     uint8_t *valid;
-    uint64_t *bitmap;      // pooling candidates of the current chunk
-    uint32_t *wcount;      // popcount per bitmap word
-    uint32_t *woff;        // exclusive prefix of wcount (nwords + 1)
-    CandHdr *chdr;         // compacted candidates, ascending cell index
-    CandVal *cval;
+    PoolTouch *ptouch;     // pooling sweep: per-cell touch record
+    int2 *ptpos;           // pooling sweep: in-chunk run bounds in P
+    // ring of NB per-chunk candidate buffers (chunk ch uses buffer ch % NB):
+    uint64_t *bm_ring;     // candidate bitmap (nwords per buffer)
+    uint32_t *wc_ring;     // popcount per bitmap word (nwords per buffer)
+    uint32_t *wo_ring;     // exclusive prefix of wc (nwords + 1 per buffer)
+    CandHdr *hdr_ring;     // compacted candidates, ascending cell index (WH per buffer)
+    CandVal *val_ring;
     int64_t nwords;
+    int NB, C2;            // ring size, events per pooling chunk
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // outputs
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
@@ -267,6 +280,19 @@ __global__ void k_touch(Ctx c, int c0, int c1, uint32_t seq) {
         }
     }
     if (nx >= c1) c.tpos[q].y = c.pos[e];
+}
+
+// Pooling sweep: first in-chunk event of every touched cell and its run bounds.
+__global__ void k_touch_pool(Ctx c, int c0, int c1, uint32_t seq) {
+    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c1) return;
+    const uint32_t q = c.pix[e];
+    const int nx = c.next[e];
+    if (c.prev[e] < c0) {
+        c.ptouch[q] = PoolTouch{seq, (uint32_t)e | (nx < c1 ? 0x80000000u : 0u)};
+        c.ptpos[q].x = c.pos[e];
+    }
+    if (nx >= c1) c.ptpos[q].y = c.pos[e];
 }
 
 // SAE snapshot <- last event of the chunk at each touched pixel.
@@ -597,15 +623,15 @@ __global__ __launch_bounds__(256) void k_fit_generic(Ctx c, uint32_t seq) {
 }
 
 // ---------------------------------------------------------------------------
-// Candidate-cell bitmap for pooling chunk [c0, c1): bit q set if q is touched in
-// the chunk, or its snapshot flow is valid and within the kill time of some
-// event of the chunk (a superset of every cell that can contribute to any event
-// of the chunk).  One wave ballot per 64 cells, popcount per word.
-__global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq) {
+// Candidate-cell bitmap for pooling chunk `chunk_idx` into ring buffer b: bit q
+// set if q is touched in the chunk, or its snapshot flow is valid and within the
+// kill time of some event of the chunk (a superset of every cell that can
+// contribute to any event of the chunk).  One wave ballot per 64 cells.
+__global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq, int b) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = false;
     if (q < c.WH) {
-        act = (c.cells[q].tag & kSeqMask) == seq;
+        act = c.ptouch[q].seq == seq;
         if (!act) {
             const int64_t ft = c.ftime[q];
             const int64_t lo = (int64_t)c.ctmin[chunk_idx] - (int64_t)kKillUs;
@@ -613,76 +639,97 @@ __global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq) {
             act = ft >= 0 && ft > lo && ft < hi;
         }
     }
-    const uint64_t b = __ballot(act);
+    const uint64_t bal = __ballot(act);
     if ((threadIdx.x & 63) == 0 && (q >> 6) < c.nwords) {
-        c.bitmap[q >> 6] = b;
-        c.wcount[q >> 6] = (uint32_t)__popcll(b);
+        c.bm_ring[(int64_t)b * c.nwords + (q >> 6)] = bal;
+        c.wc_ring[(int64_t)b * c.nwords + (q >> 6)] = (uint32_t)__popcll(bal);
     }
 }
 
-// Exclusive prefix of the per-word popcounts (single workgroup of 1024).
-__global__ __launch_bounds__(1024) void k_scan(Ctx c) {
-    __shared__ uint32_t part[1024];
+// Exclusive prefix of buffer b's per-word popcounts (single workgroup of 1024):
+// per-thread serial sums, wave scans, one LDS pass over the 16 wave totals.
+__global__ __launch_bounds__(1024) void k_scan(Ctx c, int b) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t *wc = c.wc_ring + (int64_t)b * c.nwords;
+    uint32_t *wo = c.wo_ring + (int64_t)b * (c.nwords + 1);
     const int64_t nw = c.nwords;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t per = (nw + 1023) / 1024;
-    const int64_t b = tid * per, e = b + per < nw ? b + per : nw;
+    const int64_t w0 = tid * per, w1 = w0 + per < nw ? w0 + per : nw;
     uint32_t sum = 0;
-    for (int64_t w = b; w < e; ++w) sum += c.wcount[w];
-    part[tid] = sum;
+    for (int64_t w = w0; w < w1; ++w) sum += wc[w];
+    uint32_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = tid >= off ? part[tid - off] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    uint32_t base = 0;
+    for (int k = 0; k < wv; ++k) base += wsum[k];
+    uint32_t run = base + incl - sum;
+    for (int64_t w = w0; w < w1; ++w) {
+        wo[w] = run;
+        run += wc[w];
     }
-    uint32_t run = tid ? part[tid - 1] : 0u;
-    for (int64_t w = b; w < e; ++w) {
-        c.woff[w] = run;
-        run += c.wcount[w];
-    }
-    if (tid == 1023) c.woff[nw] = part[1023];
+    if (tid == 1023) wo[nw] = run;
 }
 
-// Candidate index of the first candidate with cell index >= L.
-__device__ __forceinline__ uint32_t cand_index(const Ctx &c, int64_t L) {
+// Candidate index (in buffer b) of the first candidate with cell index >= L.
+__device__ __forceinline__ uint32_t cand_index(const Ctx &c, int b, int64_t L) {
     const int64_t w = L >> 6;
     const int r = (int)(L & 63);
-    uint32_t k = c.woff[w];
-    if (r) k += (uint32_t)__popcll(c.bitmap[w] & ((1ull << r) - 1));
+    uint32_t k = c.wo_ring[(int64_t)b * (c.nwords + 1) + w];
+    if (r) k += (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((1ull << r) - 1));
     return k;
 }
 
-// Materialise the candidate records of the chunk (thread per cell).
-__global__ void k_fill(Ctx c, uint32_t seq) {
+// Materialise the candidate records of the chunk into buffer b (thread per cell).
+__global__ void k_fill(Ctx c, uint32_t seq, int b) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= c.WH) return;
-    const uint64_t bits = c.bitmap[q >> 6];
+    const uint64_t bits = c.bm_ring[(int64_t)b * c.nwords + (q >> 6)];
     const int r = (int)(q & 63);
     if (!((bits >> r) & 1)) return;
-    const uint32_t k = c.woff[q >> 6] + (uint32_t)__popcll(bits & ((1ull << r) - 1));
-    const SaeCell s = c.cells[q];
+    const uint32_t k = c.wo_ring[(int64_t)b * (c.nwords + 1) + (q >> 6)] +
+                       (uint32_t)__popcll(bits & ((1ull << r) - 1));
+    const PoolTouch pt = c.ptouch[q];
     const FlowCell snap = c.fsnap[q];
     CandHdr hd;
     CandVal v;
     hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
     hd.t_snap = snap.t;
     v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
-    if ((s.tag & kSeqMask) == seq) {
-        const int e1 = (int)(s.e1m & kSeqMask);
+    if (pt.seq == seq) {
+        const int e1 = (int)(pt.e1m & kSeqMask);
         const FlowCell f1 = c.evf[e1];
+        const int2 run = c.ptpos[q];
         hd.e1 = e1;
-        hd.lin |= (s.e1m & 0x80000000u ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
+        hd.lin |= (pt.e1m & 0x80000000u ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
         hd.t1 = f1.t;
         v.L1 = f1.L; v.Lc1 = f1.Lc; v.Ls1 = f1.Ls;
+        v.run_lo = run.x; v.run_hi = run.y;
     } else {
         hd.e1 = INT_MAX;
         hd.t1 = 0;
         v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
+        v.run_lo = 0; v.run_hi = 0;
     }
-    c.chdr[k] = hd;
-    c.cval[k] = v;
+    const int64_t kb = (int64_t)b * c.WH + k;
+    c.hdr_ring[kb] = hd;
+    c.val_ring[kb] = v;
+}
+
+// Last event with id <= e over a candidate's in-chunk run P[lo..hi] (P[lo] <= e).
+__device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, int e) {
+    if (c.P[hi] <= e) return hi;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (c.P[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
 }
 
 // Butterfly sums over the 64 lanes: quad xor-1, xor-2, row half-mirror and
@@ -733,7 +780,7 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 // bitwise independent of chunking and streaming splits, and identical
 // contributor sets give identical scale sums (tie rule of vFlow.cpp:1161).
 template <int K>
-__global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t seq) {
+__global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     __shared__ int s_pre[4][130];       // per wave: prefix of candidate counts over rows
     __shared__ int s_a[4][128];         // per wave: first candidate of each row
     __shared__ uint2 s_con[4][kPoolCap];  // per wave: contributors {ref, kind | k0 << 8}
@@ -742,6 +789,9 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
     if (w >= c1) return;
     const int e = c.Q[w];  // events of the chunk in tile order
     if (!c.valid[e]) return;
+    const int buf = (w / c.C2) % c.NB;  // this event's chunk's candidate buffer
+    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.WH;
+    const CandVal *cval = c.val_ring + (int64_t)buf * c.WH;
     const int ex = c.x[e], ey = c.y[e];
     if (ex < c.own_lo || ex >= c.own_hi) return;  // halo event: fitted, pooled by its owner
     const uint32_t teu = c.t[e];
@@ -765,8 +815,8 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
             if (l0 < 0) l0 = 0;               // outside the stored region: never visited
             if (l1 > WHl - 1) l1 = WHl - 1;
             if (l0 <= l1) {
-                a = (int)cand_index(c, l0);
-                cnt = (int)cand_index(c, l1 + 1) - a;
+                a = (int)cand_index(c, buf, l0);
+                cnt = (int)cand_index(c, buf, l1 + 1) - a;
             }
             s_a[wv][r] = a;
         }
@@ -801,12 +851,12 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
         // is resolved
         int rc = 0, kc = 0;
         CandHdr hc{};
-        if (lane < total) { locate(lane, rc, kc); hc = c.chdr[kc]; }
+        if (lane < total) { locate(lane, rc, kc); hc = chdr[kc]; }
         for (int f0 = 0; f0 < total; f0 += 64) {
             const int f = f0 + lane, fn = f + 64;
             int rn = 0, kn = 0;
             CandHdr hn{};
-            if (fn < total) { locate(fn, rn, kn); hn = c.chdr[kn]; }
+            if (fn < total) { locate(fn, rn, kn); hn = chdr[kn]; }
             bool con = false;
             uint32_t ref = 0, meta = 0;
             if (f < total) {
@@ -815,7 +865,8 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
                 if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; kind = 0; ref = (uint32_t)kc; }
                 else if (!(hc.lin & kCandMore)) { ok = (hc.lin & kCandOneOk) != 0; tq = hc.t1; kind = 1; ref = (uint32_t)kc; }
                 else {  // several events at the cell inside the chunk: search its run
-                    const int sev = c.P[run_search(c, hc.lin & kCandLinMask, e)];
+                    const CandVal &cv = cval[kc];
+                    const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
                     const FlowCell fe = c.evf[sev];
                     ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)sev;
                 }
@@ -846,8 +897,8 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1, uint32_t se
     };
     auto value_of = [&](uint2 en, double &L, double &Lc, double &Ls) {
         const uint32_t kind = en.y & 0xFF;
-        if (kind == 0) { const CandVal &v = c.cval[en.x]; L = v.L_snap; Lc = v.Lc_snap; Ls = v.Ls_snap; }
-        else if (kind == 1) { const CandVal &v = c.cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
+        if (kind == 0) { const CandVal &v = cval[en.x]; L = v.L_snap; Lc = v.Lc_snap; Ls = v.Ls_snap; }
+        else if (kind == 1) { const CandVal &v = cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
         else { const FlowCell fe = c.evf[en.x]; L = fe.L; Lc = fe.Lc; Ls = fe.Ls; }
     };
     // ---- phase B1: mean length per scale; lane l takes a contiguous share of
@@ -992,12 +1043,17 @@ struct farms_handle {
     int2 *tpos = nullptr;
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    // per pooling chunk
-    uint64_t *bitmap = nullptr;
-    uint32_t *wcount = nullptr, *woff = nullptr;
-    CandHdr *chdr = nullptr;
-    CandVal *cval = nullptr;
+    PoolTouch *ptouch = nullptr;
+    int2 *ptpos = nullptr;
+    // ring of per-chunk candidate buffers (NB = 2 x pool_batch)
+    int pool_batch = 8, NB = 16;
+    uint64_t *bm_ring = nullptr;
+    uint32_t *wc_ring = nullptr, *wo_ring = nullptr;
+    CandHdr *hdr_ring = nullptr;
+    CandVal *val_ring = nullptr;
     int64_t nwords = 0;
+    hipStream_t s_chain = nullptr, s_pool = nullptr;  // candidate-building chain, pooling kernels
+    std::vector<hipEvent_t> sync_ev;                  // dependency events (no timing)
     uint32_t seq = 0;
     // per-call workspace
     int64_t cap = 0;
@@ -1092,18 +1148,19 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipMemsetAsync(h->tpos, 0, sizeof(int2) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->ptouch, 0, sizeof(PoolTouch) * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     return FARMS_OK;
 }
 
 template <int K>
-void launch_pool(const Ctx &c, int c0, int c1, uint32_t seq, hipStream_t s) {
+void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), 0, s, c, c0, c1, seq);
+    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), 0, s, c, c0, c1);
 }
 
-typedef void (*pool_launcher)(const Ctx &, int, int, uint32_t, hipStream_t);
+typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
 pool_launcher pool_for(int K) {
     switch (K) {
     case 1: return launch_pool<1>;   case 2: return launch_pool<2>;   case 3: return launch_pool<3>;
@@ -1135,6 +1192,15 @@ int ensure_kernel_events(farms_handle *h, size_t count) {
     return FARMS_OK;
 }
 
+int ensure_sync_events(farms_handle *h, size_t count) {
+    while (h->sync_ev.size() < count) {
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        h->sync_ev.push_back(ev);
+    }
+    return FARMS_OK;
+}
+
 // The whole per-event loop for n device-resident events.
 int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
              int64_t n64, farms_records *dout) {
@@ -1150,7 +1216,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.Q = h->Q;
     c.cells = h->cells; c.tpos = h->tpos; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
-    c.bitmap = h->bitmap; c.wcount = h->wcount; c.woff = h->woff; c.chdr = h->chdr; c.cval = h->cval; c.nwords = h->nwords;
+    c.ptouch = h->ptouch; c.ptpos = h->ptpos;
+    c.bm_ring = h->bm_ring; c.wc_ring = h->wc_ring; c.wo_ring = h->wo_ring;
+    c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
+    c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
@@ -1162,12 +1231,25 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
 
     const bool prof = h->profiling;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
+    const int B = h->pool_batch;
+    const int n_super = ceil_div(n_pool_chunks, B);
     if (prof) {
-        int rc = ensure_kernel_events(h, 2 * (size_t)(n_fit_chunks + n_pool_chunks));
+        int rc = ensure_kernel_events(h, 2 * (size_t)(n_fit_chunks + n_super));
         if (rc) return rc;
         HIPCHK(hipEventRecord(h->ev[0], s));
     }
-    // ---- prep: validate, pixel ids, sort by pixel, links
+    // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
+    // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
+    {
+        int rc = ensure_sync_events(h, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
+        if (rc) return rc;
+    }
+    hipEvent_t ev_prep = h->sync_ev[0];
+    auto ev_fit = [&](int f) { return h->sync_ev[1 + f]; };
+    auto ev_cand = [&](int S) { return h->sync_ev[1 + n_fit_chunks + 2 * S]; };
+    auto ev_pool = [&](int S) { return h->sync_ev[2 + n_fit_chunks + 2 * S]; };
+
+    // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
     HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->wkey, h->err,
                        h->pool_chunk, h->tile_bits);
@@ -1180,19 +1262,18 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
                                               end_bit_for(h->WH), s));
     hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next);
     {
-        const int nchunks = ceil_div(n, h->pool_chunk);
         int cb = 1;
-        while ((1 << cb) < nchunks) ++cb;
+        while ((1 << cb) < n_pool_chunks) ++cb;
         if (cb + h->tile_bits > 32) return fail(FARMS_EINVAL, "too many pooling chunks for one call; raise pool_chunk");
         size_t b2 = h->cub_bytes;
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, b2, h->wkey, h->wkey_sorted, h->iota, h->Q, n, 0,
                                                   h->tile_bits + cb, s));
     }
-    const int nch = ceil_div(n, h->pool_chunk);
-    hipLaunchKernelGGL(k_chunk_minmax, dim3(nch), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
+    hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
+    HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
 
-    // ---- sweep 1: local plane fits
+    // ---- sweep 1 (stream F): local plane fits, chunk after chunk
     int fit_launches = 0;
     for (int c0 = 0; c0 < n; c0 += h->fit_chunk) {
         const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->fit_chunk, n);
@@ -1205,33 +1286,56 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         if (h->fr >= 1 && h->fr <= 3)
             hipLaunchKernelGGL(k_fit_generic, g, b, 0, s, c, seq);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches + 1], s));
+        HIPCHK(hipEventRecord(ev_fit(fit_launches), s));
         hipLaunchKernelGGL(k_sae_update, g, b, 0, s, c, c0, c1);
         ++fit_launches;
     }
     HIPCHK(hipGetLastError());
     if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
 
-    // ---- sweep 2: multiscale pooling
+    // ---- sweep 2: candidate lists on stream C (a serial chain over chunks,
+    // each chunk into ring buffer ch % NB), pooling kernels on stream P, one
+    // launch per super-chunk of B chunks.  Pooling of a chunk reads only its
+    // candidate buffer, the per-event flows and P, so it overlaps the chain of
+    // later chunks and the fit sweep.
+    hipStream_t sc = h->s_chain, sp = h->s_pool;
     pool_launcher pl = pool_for(h->K);
-    int pool_launches = 0;
     const int bm_blocks = ceil_div(h->nwords * 64, 256);
     const int cell_blocks = ceil_div(h->WH, 256);
-    for (int ch = 0, c0 = 0; c0 < n; ++ch, c0 += h->pool_chunk) {
-        const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->pool_chunk, n);
-        const uint32_t seq = ++h->seq;
-        const dim3 g(ceil_div(c1 - c0, 256)), b(256);
-        hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
-        hipLaunchKernelGGL(k_bitmap, dim3(bm_blocks), dim3(256), 0, s, c, ch, seq);
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, c);
-        hipLaunchKernelGGL(k_fill, dim3(cell_blocks), dim3(256), 0, s, c, seq);
-        const size_t ke = 2 * ((size_t)n_fit_chunks + pool_launches);
-        if (prof) HIPCHK(hipEventRecord(h->kev[ke], s));
-        pl(c, c0, c1, seq, s);
-        if (prof) HIPCHK(hipEventRecord(h->kev[ke + 1], s));
-        hipLaunchKernelGGL(k_flow_update, g, b, 0, s, c, c0, c1);
-        ++pool_launches;
+    HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
+    int fit_waited = -1;
+    for (int S = 0; S < n_super; ++S) {
+        const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
+        if (S >= 2) HIPCHK(hipStreamWaitEvent(sc, ev_pool(S - 2), 0));  // ring buffers of S-2 are free
+        for (int ch = ch0; ch < ch1; ++ch) {
+            const int c0 = ch * h->pool_chunk;
+            const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->pool_chunk, n);
+            const int f = c0 / h->fit_chunk;  // fit chunks are whole pooling chunks
+            if (f > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(f), 0)); fit_waited = f; }
+            const uint32_t seq = ++h->seq;
+            const int buf = ch % h->NB;
+            const dim3 g(ceil_div(c1 - c0, 256)), b(256);
+            hipLaunchKernelGGL(k_touch_pool, g, b, 0, sc, c, c0, c1, seq);
+            hipLaunchKernelGGL(k_bitmap, dim3(bm_blocks), dim3(256), 0, sc, c, ch, seq, buf);
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, sc, c, buf);
+            hipLaunchKernelGGL(k_fill, dim3(cell_blocks), dim3(256), 0, sc, c, seq, buf);
+            hipLaunchKernelGGL(k_flow_update, g, b, 0, sc, c, c0, c1);
+        }
+        HIPCHK(hipEventRecord(ev_cand(S), sc));
+        HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
+        const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
+        pl(c, p0, p1, sp);
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
+        HIPCHK(hipEventRecord(ev_pool(S), sp));
     }
+    const int pool_launches = n_super;
     HIPCHK(hipGetLastError());
+    // join: stream F waits for the last chain step and the last pooling launch
+    if (n_super > 0) {
+        HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
+        HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
+    }
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (prof) {
         HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 5, s));
@@ -1248,8 +1352,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         float a = 0, b = 0, d = 0;
         HIPCHK(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
         HIPCHK(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
-        HIPCHK(hipEventElapsedTime(&d, h->ev[2], h->ev[3]));
-        st.ms_prep = a; st.ms_fit = b; st.ms_pool = d; st.ms_total = (double)a + b + d;
+        HIPCHK(hipEventElapsedTime(&d, h->ev[1], h->ev[3]));
+        // the fit and pooling sweeps overlap: ms_pool spans from the end of prep
+        // to the end of the last pooling launch
+        st.ms_prep = a; st.ms_fit = b; st.ms_pool = d; st.ms_total = (double)a + d;
         double kf = 0, kp = 0;
         for (int i = 0; i < fit_launches; ++i) {
             float v = 0;
@@ -1258,7 +1364,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         for (int i = 0; i < pool_launches; ++i) {
             float v = 0;
-            const size_t ke = 2 * ((size_t)n_fit_chunks + i);
+            const size_t ke = 2 * ((size_t)n_fit_chunks + i);  // one k_pool launch per super-chunk
             HIPCHK(hipEventElapsedTime(&v, h->kev[ke], h->kev[ke + 1]));
             kp += v;
         }
@@ -1325,6 +1431,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->J = prm->window_jump; h->M = prm->max_window; h->K = K;
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
+    if (prm->pool_batch > 0) h->pool_batch = prm->pool_batch;
+    h->NB = 2 * h->pool_batch;
     h->nwords = (h->WH + 63) / 64;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
@@ -1334,14 +1442,17 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     }
     int rc = FARMS_OK;
     auto bail = [&](int code) { farms_destroy(h); return code; };
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->s_chain, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->s_pool, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->tpos, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->bitmap, h->nwords)) ||
-        (rc = dalloc(&h->wcount, h->nwords)) || (rc = dalloc(&h->woff, h->nwords + 1)) ||
-        (rc = dalloc(&h->chdr, h->WH)) || (rc = dalloc(&h->cval, h->WH)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->defer_count, 1)) || (rc = dalloc(&h->counters, 8)))
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ptouch, h->WH)) || (rc = dalloc(&h->ptpos, h->WH)) ||
+        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || (rc = dalloc(&h->wc_ring, h->nwords * h->NB)) ||
+        (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->WH * h->NB)) ||
+        (rc = dalloc(&h->val_ring, h->WH * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->defer_count, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
@@ -1351,12 +1462,18 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
 extern "C" int farms_destroy(farms_handle *h) {
     if (!h) return FARMS_OK;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
+    if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     free_workspace(h);
     dfree(h->cells); dfree(h->tpos); dfree(h->ftime); dfree(h->fsnap);
-    dfree(h->bitmap); dfree(h->wcount); dfree(h->woff); dfree(h->chdr); dfree(h->cval); dfree(h->err); dfree(h->defer_count); dfree(h->counters);
+    dfree(h->ptouch); dfree(h->ptpos); dfree(h->bm_ring); dfree(h->wc_ring); dfree(h->wo_ring);
+    dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->defer_count); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);
+    for (auto &ev : h->sync_ev) (void)hipEventDestroy(ev);
+    if (h->s_pool) (void)hipStreamDestroy(h->s_pool);
+    if (h->s_chain) (void)hipStreamDestroy(h->s_chain);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return FARMS_OK;

@@ -51,6 +51,7 @@ class FarmsParams(ctypes.Structure):
         ("region_width", ctypes.c_int32),
         ("own_x0", ctypes.c_int32),
         ("own_x1", ctypes.c_int32),
+        ("pool_batch", ctypes.c_int32),
     ]
 
 
@@ -265,7 +266,8 @@ class FlowManager:
 
     def __init__(self, height: int = 320, width: int = 320, filter_size: int = 3, min_evts_on_plane: int = 5,
                  window_jump: int = 5, max_window: int = 50, device: int = 0, fit_chunk: int = 0,
-                 pool_chunk: int = 0, region: tuple | None = None, owned: tuple | None = None):
+                 pool_chunk: int = 0, region: tuple | None = None, owned: tuple | None = None,
+                 pool_batch: int = 0):
         self._lib = load_hip_library()
         prm = FarmsParams()
         _check(self._lib, self._lib.farms_default_params(ctypes.byref(prm)))
@@ -273,6 +275,7 @@ class FlowManager:
         prm.filter_size, prm.min_inliers = int(filter_size), int(min_evts_on_plane)
         prm.window_jump, prm.max_window = int(window_jump), int(max_window)
         prm.device, prm.fit_chunk, prm.pool_chunk = int(device), int(fit_chunk), int(pool_chunk)
+        prm.pool_batch = int(pool_batch)
         if region is not None:  # (x0, x1): stored columns
             prm.region_x0, prm.region_width = int(region[0]), int(region[1]) - int(region[0])
         if owned is not None:  # (x0, x1): pooled columns

@@ -35,6 +35,7 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <cstdlib>
 
 #include "../../include/farms_hip.h"
 
@@ -58,8 +59,8 @@ int fail(int code, const std::string &msg) {
 constexpr double kMaxStamp = 4294967296.0;  // vFlow.h:27
 constexpr double kTsToSec = 1e-6;           // vFlow.h:28
 constexpr double kKillUs = 500.0;           // vFlow.cpp:961
-constexpr int kDefaultFitChunk = 1 << 18;
-constexpr int kDefaultPoolChunk = 1 << 15;
+constexpr int kDefaultFitChunk = 1 << 16;
+constexpr int kDefaultPoolChunk = 1 << 14;
 constexpr int kMaxScales = 16;
 
 // Local-flow state of one event, and the flow surface cell (x-major).  L = 0 for
@@ -140,12 +141,13 @@ struct Ctx {
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
     uint8_t *valid;
-    PoolTouch *ptouch;     // pooling sweep: per-cell touch record
-    int2 *ptpos;           // pooling sweep: in-chunk run bounds in P
+    PoolTouch *ptouch;     // pooling sweep: per-cell touch record, 3 x WH (by chunk % 3)
+    int2 *ptpos;           // pooling sweep: in-chunk run bounds in P, 3 x WH
     // ring of NB per-chunk candidate buffers (chunk ch uses buffer ch % NB):
     uint64_t *bm_ring;     // candidate bitmap (nwords per buffer)
-    uint32_t *wc_ring;     // popcount per bitmap word (nwords per buffer)
-    uint32_t *wo_ring;     // exclusive prefix of wc (nwords + 1 per buffer)
+    uint32_t *blk_ring;    // candidates per 1024-cell block (nblk per buffer)
+    uint32_t *wo_ring;     // candidates before each bitmap word (nwords + 1 per buffer)
+    int nblk;
     CandHdr *hdr_ring;     // compacted candidates, ascending cell index (WH per buffer)
     CandVal *val_ring;
     int64_t nwords;
@@ -157,8 +159,6 @@ struct Ctx {
     int32_t *ox, *oy, *ot, *op;
     unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells [3] cand [4] contrib
     int2 *dbg_tc;                  // profiling only: per event (candidates scanned, contributors)
-    int32_t *defer;                // events whose fit needs the generic path
-    int *defer_count;
 };
 
 // ---------------------------------------------------------------------------
@@ -194,6 +194,26 @@ __device__ __forceinline__ int64_t sae_resolve(const Ctx &c, const SaeCell &s, u
         }
     }
     return (s.tag >> 31) ? (int64_t)s.tsnap : int64_t(-1);
+}
+
+// Fast-path form: h is the cell's first 16 B (tag, e1m, t1, tsnap); the
+// second inline event is loaded only when it decides the answer.
+__device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint4 h, uint32_t q, int e, uint32_t seq) {
+    if ((h.x & kSeqMask) == seq) {
+        const int e1 = (int)(h.y & kSeqMask);
+        if (e1 <= e) {
+            if (!(h.y >> 31)) return (int64_t)h.z;
+            const uint2 g = reinterpret_cast<const uint2 *>(c.cells)[4 * (size_t)q + 2];  // e2m, t2
+            if ((int)(g.x & kSeqMask) > e) return (int64_t)h.z;
+            if (!(g.x >> 31)) return (int64_t)g.y;
+            return -2;
+        }
+    }
+    return (h.x >> 31) ? (int64_t)h.w : int64_t(-1);
+}
+
+__device__ __forceinline__ uint4 sae_head(const Ctx &c, uint32_t q) {
+    return reinterpret_cast<const uint4 *>(c.cells)[2 * (size_t)q];
 }
 
 __device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
@@ -260,16 +280,36 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
     }
 }
 
-// Record, for every pixel touched by chunk [c0, c1), its first in-chunk event
-// (inline in the SAE cell) and the bounds of its in-chunk run in P.
-__global__ void k_touch(Ctx c, int c0, int c1, uint32_t seq) {
-    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+// Fit sweep, between chunks (one launch): for chunk f = [c0, c1), record at
+// every touched pixel its first two in-chunk events inline and the bounds of
+// its in-chunk run in P, and set the SAE snapshot to the pixel's last event
+// before the chunk (prev of its first event); for chunk f-1 = [p0, c0), set
+// the snapshot of pixels it touched that chunk f does not touch.  The two
+// parts write disjoint cells.
+__global__ void k_fit_prep(Ctx c, int p0, int c0, int c1, uint32_t seq) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ep = p0 + i;
+    if (ep < c0) {
+        const int nx = c.next[ep];
+        if (nx >= c0 && nx >= c1) {  // last event of chunk f-1 at a pixel chunk f does not touch
+            SaeCell *cell = &c.cells[c.pix[ep]];
+            cell->tag |= 0x80000000u;
+            cell->tsnap = c.t[ep];
+        }
+    }
+    const int e = c0 + i;
     if (e >= c1) return;
     const uint32_t q = c.pix[e];
     const int nx = c.next[e];
     if (c.prev[e] < c0) {  // first event of the pixel in the chunk
         SaeCell *cell = &c.cells[q];
-        cell->tag = (cell->tag & ~kSeqMask) | seq;
+        const int pv = c.prev[e];
+        if (pv >= 0) {
+            cell->tag = seq | 0x80000000u;
+            cell->tsnap = c.t[pv];
+        } else {  // no earlier event in this call: keep the snapshot of earlier calls
+            cell->tag = (cell->tag & 0x80000000u) | seq;
+        }
         cell->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
         cell->t1 = c.t[e];
         c.tpos[q].x = c.pos[e];
@@ -280,42 +320,6 @@ __global__ void k_touch(Ctx c, int c0, int c1, uint32_t seq) {
         }
     }
     if (nx >= c1) c.tpos[q].y = c.pos[e];
-}
-
-// Pooling sweep: first in-chunk event of every touched cell and its run bounds.
-__global__ void k_touch_pool(Ctx c, int c0, int c1, uint32_t seq) {
-    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= c1) return;
-    const uint32_t q = c.pix[e];
-    const int nx = c.next[e];
-    if (c.prev[e] < c0) {
-        c.ptouch[q] = PoolTouch{seq, (uint32_t)e | (nx < c1 ? 0x80000000u : 0u)};
-        c.ptpos[q].x = c.pos[e];
-    }
-    if (nx >= c1) c.ptpos[q].y = c.pos[e];
-}
-
-// SAE snapshot <- last event of the chunk at each touched pixel.
-__global__ void k_sae_update(Ctx c, int c0, int c1) {
-    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= c1) return;
-    if (c.next[e] >= c1) {
-        SaeCell *cell = &c.cells[c.pix[e]];
-        cell->tag |= 0x80000000u;
-        cell->tsnap = c.t[e];
-    }
-}
-
-// Flow snapshot <- last event of the chunk at each touched pixel.
-__global__ void k_flow_update(Ctx c, int c0, int c1) {
-    const int e = c0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= c1) return;
-    if (c.next[e] >= c1) {
-        const uint32_t q = c.pix[e];
-        const FlowCell f = c.evf[e];
-        c.fsnap[q] = f;
-        c.ftime[q] = f.L > 0 ? (int64_t)f.t : -1;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -357,217 +361,334 @@ __device__ __forceinline__ double det3_partialpivlu(const double a[9]) {
 }
 
 // ---------------------------------------------------------------------------
-// Local plane fit of one event (computeLocalFlow + computeGrads).  FR > 0:
-// fRad known at compile time, fully unrolled, cell stamps kept in registers;
-// returns false (nothing written) if some pixel fired 3+ times in the chunk
-// and needs its run searched — the generic FR == 0 instance then redoes the
-// event out of line.  FR == 0: any fRad, every lookup complete.
-template <int FR>
-__device__ __forceinline__ bool fit_event(const Ctx &c, int e, uint32_t seq, double &vx_out, double &vy_out) {
-    constexpr bool FAST = FR > 0;
-    const int fr = FR > 0 ? FR : c.fr;
+// Local plane fit of one event (computeLocalFlow + computeGrads, vFlow.cpp:
+// 863-942, 1290-1380) for any fRad, every lookup complete, one thread.  Used
+// for very large filters only (k_fit_wave stages smaller ones in LDS).
+__device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_out, double &vy_out) {
+    const int fr = c.fr;
     const int side = 2 * fr + 1;
     const int np = side * side;
     const int W = c.W, H = c.H;
     const int ex = c.x[e], ey = c.y[e];
     const uint32_t te = c.t[e];
-    double vx = 0.0, vy = 0.0;
-
+    vx_out = 0.0;
+    vy_out = 0.0;
     // ---- window scores (vFlow.cpp:870-912): sum over the window of
     // (t_e - t_k) + 2^32 [t_k > t_e], exact as int64; ties: first strict min.
     bool wok[9];
     int64_t score[9];
     bool any = false;
-#pragma unroll
     for (int w = 0; w < 9; ++w) {
         const int ci = ex + (w / 3 - 1) * fr, cj = ey + (w % 3 - 1) * fr;
         wok[w] = ci - fr >= 0 && ci + fr <= W - 1 && cj - fr >= 0 && cj + fr <= H - 1;
         score[w] = 0;
         any |= wok[w];
     }
-    if (!any) { vx_out = 0.0; vy_out = 0.0; return true; }
-    bool slow = false;
-    if (FR > 0) {
-        // union of the 9 windows, one column (fixed du) at a time: the column's
-        // cells are loaded together, then resolved
-        constexpr int US = FR > 0 ? 4 * FR + 1 : 1;
-#pragma unroll
-        for (int du = -2 * FR; du <= 2 * FR; ++du) {
-            const int u = ex + du;
-            if (u < 0 || u >= W) continue;
-            const bool inr = u >= c.X0 && u < c.XR1;  // outside the stored region: never visited
-            SaeCell col[US];
-            const int cbase = (u - c.X0) * H + ey;
-#pragma unroll
-            for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
-                const int v = ey + dv;
-                col[dv + 2 * FR] = SaeCell{};
-                if (inr && v >= 0 && v < H) col[dv + 2 * FR] = c.cells[cbase + dv];
+    if (!any) return;
+    auto stamp = [&](int u, int v) -> int64_t {
+        return (u >= c.X0 && u < c.XR1) ? sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq) : int64_t(-1);
+    };
+    for (int du = -2 * fr; du <= 2 * fr; ++du) {
+        const int u = ex + du;
+        if (u < 0 || u >= W) continue;
+        for (int dv = -2 * fr; dv <= 2 * fr; ++dv) {
+            const int v = ey + dv;
+            if (v < 0 || v >= H) continue;
+            int mask = 0;
+            for (int w = 0; w < 9; ++w) {
+                const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
+                if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
             }
-#pragma unroll
-            for (int dv = -2 * FR; dv <= 2 * FR; ++dv) {
-                const int v = ey + dv;
-                if (v < 0 || v >= H) continue;
-                int mask = 0;
-#pragma unroll
-                for (int w = 0; w < 9; ++w) {
-                    const int ou = (w / 3 - 1) * FR, ov = (w % 3 - 1) * FR;
-                    if (du - ou <= FR && ou - du <= FR && dv - ov <= FR && ov - dv <= FR && wok[w]) mask |= 1 << w;
-                }
-                if (!mask) continue;
-                const int64_t st = sae_resolve<FAST>(c, col[dv + 2 * FR], (uint32_t)(cbase + dv), e, seq);
-                slow |= st == -2;
-                const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-                const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
-#pragma unroll
-                for (int w = 0; w < 9; ++w)
-                    if (mask & (1 << w)) score[w] += d;
-            }
-        }
-        if (slow) return false;
-    } else {
-        for (int du = -2 * fr; du <= 2 * fr; ++du) {
-            const int u = ex + du;
-            if (u < 0 || u >= W) continue;
-            for (int dv = -2 * fr; dv <= 2 * fr; ++dv) {
-                const int v = ey + dv;
-                if (v < 0 || v >= H) continue;
-                int mask = 0;
-#pragma unroll
-                for (int w = 0; w < 9; ++w) {
-                    const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
-                    if (du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr && wok[w]) mask |= 1 << w;
-                }
-                if (!mask) continue;
-                const int64_t st = (u >= c.X0 && u < c.XR1) ? sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq)
-                                                            : int64_t(-1);
-                const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-                const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
-#pragma unroll
-                for (int w = 0; w < 9; ++w)
-                    if (mask & (1 << w)) score[w] += d;
-            }
+            if (!mask) continue;
+            const int64_t st = stamp(u, v);
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+            for (int w = 0; w < 9; ++w)
+                if (mask & (1 << w)) score[w] += d;
         }
     }
-    // bestscore starts at MAXSTAMP + 1; sums compare exactly
     const int64_t nn = np;
-    int64_t best = nn * ((int64_t(1) << 32) + 1);
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
     int bw = -1;
-#pragma unroll
     for (int w = 0; w < 9; ++w)
         if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
-    if (bw < 0 || best > nn * (int64_t(1) << 32)) { vx_out = 0.0; vy_out = 0.0; return true; }
-
-    // ---- gather the winning window, cx-major (vFlow.cpp:923-930)
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;
+    // ---- the winning window, cx-major (vFlow.cpp:923-930)
     const int bi = ex + (bw / 3 - 1) * fr, bj = ey + (bw % 3 - 1) * fr;
-    constexpr int NPC = FR > 0 ? (2 * FR + 1) * (2 * FR + 1) : 1;
-    uint32_t tks[NPC];
-    uint64_t vis = 0;
-    if (FR > 0) {  // a column at a time, loads first (all cells were resolved above)
-        constexpr int SD = 2 * FR + 1;
-#pragma unroll
-        for (int cxo = 0; cxo < SD; ++cxo) {
-            const int u = bi + cxo - FR;
-            const bool inr = u >= c.X0 && u < c.XR1;
-            const int cb = (u - c.X0) * H + (bj - FR);
-            SaeCell col[SD];
-#pragma unroll
-            for (int cyo = 0; cyo < SD; ++cyo) col[cyo] = inr ? c.cells[cb + cyo] : SaeCell{};
-#pragma unroll
-            for (int cyo = 0; cyo < SD; ++cyo) {
-                const int k = cxo * SD + cyo;
-                const int64_t st = sae_resolve<FAST>(c, col[cyo], (uint32_t)(cb + cyo), e, seq);
-                tks[k] = st < 0 ? 0u : (uint32_t)st;
-                if (st >= 0) vis |= uint64_t(1) << k;
-            }
-        }
-    }
     auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
         const int cx = bi + k / side - fr, cy = bj + k % side - fr;
-        if (FR > 0) {
-            // opaque copies: every pass re-derives X, Y, Yt from the packed
-            // stamps instead of keeping 3 x NP doubles live (register budget)
-            uint64_t vv = vis;
-            uint32_t tt = tks[k < NPC ? k : 0];
-            asm volatile("" : "+v"(tt), "+v"(vv));
-            const bool vk = (vv >> k) & 1;
-            X = vk ? cx : 0; Y = vk ? cy : 0; T = tt;
-        } else {
-            const int64_t st = (cx >= c.X0 && cx < c.XR1) ? sae_asof(c, (uint32_t)((cx - c.X0) * H + cy), e, seq)
-                                                          : int64_t(-1);
-            X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
-        }
+        const int64_t st = stamp(cx, cy);
+        X = st >= 0 ? cx : 0; Y = st >= 0 ? cy : 0; T = st >= 0 ? (uint32_t)st : 0u;
     };
     int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
-#pragma unroll
     for (int k = 0; k < np; ++k) {
         int64_t X, Y; uint32_t T;
         cell(k, X, Y, T);
         sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
     }
-    // AtA, column-major (vFlow.cpp:1311)
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};  // AtA column-major (vFlow.cpp:1311)
+    double DET = det3_partialpivlu(a);
+    if (DET < 1) return;
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+    // temp = (A2*At)*Y in Eigen's order
+    const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+    for (int k = 0; k < np; ++k) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1, m2;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+            m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+            m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+        }
+        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+    }
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+    (void)r2;
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+    for (int k = 0; k < np; ++k) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    const double speed = 1.0 / dtdp;
+    const double angle = atan2(r0, r1);
+    vx_out = speed * cos(angle);
+    vy_out = speed * sin(angle);
+}
+
+// Local plane fit of one event with fRad known at compile time (the common
+// filters 3, 5, 7): the union of the 9 candidate windows is loaded a column
+// at a time and resolved from the inline in-chunk events; cells whose pixel
+// fired 3+ times in the chunk (state past its second in-chunk event) are
+// marked and resolved afterwards by a run search in a rolled loop, so the
+// unrolled body stays small and no event leaves the kernel.  The winning
+// window's stamps go to LDS (`lt`: this thread's column, stride 256) for the
+// three passes over it.  Arithmetic is that of fit_event_generic.
+template <int FR>
+__device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq, uint32_t *lt, double &vx_out,
+                                               double &vy_out) {
+    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
+    const int W = c.W, H = c.H;
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t te = c.t[e];
+    vx_out = 0.0;
+    vy_out = 0.0;
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
+        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    if (!any) return;
+    // ---- window scores (vFlow.cpp:870-912), exact int64, first strict min.
+    // The union window is walked a column at a time (two column buffers: the
+    // next column's loads are in flight while this one is resolved); each
+    // column's stamps give three vertical partial sums, which are added to the
+    // windows whose column range contains it.  Every window's score is the
+    // same integer sum in any order.
+    uint32_t slowcol = 0;  // union columns with a cell that needs a run search
+    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+        const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
+        const int cbase = (u0 - c.X0) * H + v0;
+#pragma unroll
+        for (int i = 0; i < len; ++i) {
+            const int v = v0 + i;
+            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto score_col = [&](int du, const uint4 *col) {
+        const int u = ex + du;
+        if (u < 0 || u >= W) return;
+        int64_t dd[US];
+#pragma unroll
+        for (int i = 0; i < US; ++i) {
+            const int v = ey + i - 2 * FR;
+            dd[i] = 0;
+            if (v < 0 || v >= H) continue;
+            const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
+            if (st == -2) { slowcol |= 1u << (du + 2 * FR); continue; }
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+        }
+#pragma unroll
+        for (int ovi = 0; ovi < 3; ++ovi) {
+            int64_t sv = 0;
+#pragma unroll
+            for (int i = ovi * FR; i <= ovi * FR + 2 * FR; ++i) sv += dd[i];
+#pragma unroll
+            for (int oui = 0; oui < 3; ++oui) {
+                const int ou = (oui - 1) * FR;
+                if (du - ou <= FR && ou - du <= FR) score[oui * 3 + ovi] += sv;
+            }
+        }
+    };
+#pragma unroll 1
+    for (int du = -2 * FR; du <= 2 * FR; ++du) {
+        uint4 ca[US];
+        load_col(ex + du, ey - 2 * FR, US, ca);
+        score_col(du, ca);
+    }
+    // rare: the cells of those columns past their pixel's second in-chunk
+    // event, resolved by a run search (the column is re-read to find them)
+    while (slowcol) {
+        const int du = __builtin_ctz(slowcol) - 2 * FR;
+        slowcol &= slowcol - 1;
+        const int u = ex + du;
+        uint4 col[US];
+        load_col(u, ey - 2 * FR, US, col);
+#pragma unroll
+        for (int i = 0; i < US; ++i) {
+            const int dv = i - 2 * FR, v = ey + dv;
+            if (v < 0 || v >= H) continue;
+            const uint32_t q = (uint32_t)((u - c.X0) * H + v);
+            if (sae_resolve_h(c, col[i], q, e, seq) != -2) continue;
+            const int64_t st = sae_asof(c, q, e, seq);
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                const int ou = (w / 3 - 1) * FR, ov = (w % 3 - 1) * FR;
+                const bool in = du - ou <= FR && ou - du <= FR && dv - ov <= FR && ov - dv <= FR;
+                score[w] += d & -(int64_t)in;  // branch-free: keeps score[] in registers
+            }
+        }
+    }
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;
+
+    // ---- gather the winning window, cx-major (vFlow.cpp:923-930), into LDS
+    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
+    uint64_t vis = 0, wslow = 0;
+    auto gather_col = [&](int cxo, const uint4 *col) {
+        const int u = bi + cxo - FR;
+#pragma unroll
+        for (int cyo = 0; cyo < side; ++cyo) {
+            const int k = cxo * side + cyo;
+            const int64_t st = sae_resolve_h(c, col[cyo], (uint32_t)((u - c.X0) * H + bj - FR + cyo), e, seq);
+            const uint64_t bit = 1ull << k;
+            wslow |= st == -2 ? bit : 0ull;  // selects, not branches: vis / wslow stay in registers
+            vis |= st >= 0 ? bit : 0ull;
+            if (st != -2) lt[k * 256] = st < 0 ? 0u : (uint32_t)st;
+        }
+    };
+#pragma unroll 1
+    for (int cxo = 0; cxo < side; ++cxo) {
+        uint4 ga[side];
+        load_col(bi - FR + cxo, bj - FR, side, ga);
+        gather_col(cxo, ga);
+    }
+    while (wslow) {
+        const int k = __builtin_ctzll(wslow);
+        wslow &= wslow - 1;
+        const int u = bi + k / side - FR, v = bj + k % side - FR;
+        const int64_t st = sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq);
+        lt[k * 256] = st < 0 ? 0u : (uint32_t)st;
+        if (st >= 0) vis |= 1ull << k;
+    }
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+        const int cx = bi + k / side - FR, cy = bj + k % side - FR;
+        const bool vk = (vis >> k) & 1;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = lt[k * 256];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
+#pragma unroll 1
+    for (int k = 0; k < np; ++k) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
     const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
                          (double)sy,  (double)sx,  (double)sy, (double)np};
     double DET = det3_partialpivlu(a);
-    int inliers = 0;
-    double dtdx = 0.0, dtdy = 0.0;
-    if (!(DET < 1)) {
-        DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
-        const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
-        const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
-        const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
-        const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
-        const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
-        const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
-        const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
-        const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
-        const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
-        // temp = (A2*At)*Y in Eigen's order
-        const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
-        const double cz = (double)te * kTsToSec;
-        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < np; ++k) {
-            int64_t Xi, Yi; uint32_t T;
-            cell(k, Xi, Yi, T);
-            const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
-            const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-            double m0, m1, m2;
-            if (gemm) {
-                m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
-                m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
-                m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
-            } else {
-                m0 = (d0 * X + d3 * Y) + d6 * 1.0;
-                m1 = (d1 * X + d4 * Y) + d7 * 1.0;
-                m2 = (d2 * X + d5 * Y) + d8 * 1.0;
-            }
-            if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
-            else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+    if (DET < 1) return;  // 0 inliers
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < np; ++k) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1, m2;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+            m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+            m2 = (d2 * X + d5 * Y) + d8 * 1.0;
         }
-        if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
-        // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
-        const double dtdp = sqrt(r0 * r0 + r1 * r1);
-        const double ccx = (double)ex, ccy = (double)ey;
-#pragma unroll
-        for (int k = 0; k < np; ++k) {
-            int64_t Xi, Yi; uint32_t T;
-            cell(k, Xi, Yi, T);
-            const double Tk = (double)T;
-            const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-            const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
-            const double actualdt = yt - cz;
-            if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
-        }
-        const double speed = 1.0 / dtdp;
-        const double angle = atan2(r0, r1);
-        dtdx = speed * cos(angle);
-        dtdy = speed * sin(angle);
+        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
     }
-    if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
-    vx_out = vx;
-    vy_out = vy;
-    return true;
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+    (void)r2;
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+#pragma unroll 1
+    for (int k = 0; k < np; ++k) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    const double speed = 1.0 / dtdp;
+    const double angle = atan2(r0, r1);
+    vx_out = speed * cos(angle);
+    vy_out = speed * sin(angle);
 }
 
 // Validity gate, flow-surface value and record of one fitted event.
@@ -599,81 +720,224 @@ __device__ __forceinline__ void fit_store(const Ctx &c, int e, double vx, double
     if (c.ox) { c.ox[e] = ex; c.oy[e] = ey; c.ot[e] = (int32_t)te; c.op[e] = c.p[e]; }
 }
 
-// One thread per event of chunk [c0, c1).  Events that meet a pixel with 3+
-// in-chunk events are deferred to k_fit_generic through a small work list.
+// One thread per event of chunk [c0, c1) in tile order.
 template <int FR>
 __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq) {
+    constexpr int NPC = (2 * FR + 1) * (2 * FR + 1);
+    __shared__ uint32_t s_tk[NPC * 256];
     const int w = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c1) return;
     const int e = c.Q[w];  // chunk [c0, c1) occupies positions [c0, c1) of Q
     double vx, vy;
-    if (fit_event<FR>(c, e, seq, vx, vy)) fit_store(c, e, vx, vy);
-    else c.defer[atomicAdd(c.defer_count, 1)] = e;
-}
-
-// The deferred events (any fRad, every lookup complete); grid sized for the
-// whole chunk, the list length is read on the device.
-__global__ __launch_bounds__(256) void k_fit_generic(Ctx c, uint32_t seq) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *c.defer_count) return;
-    const int e = c.defer[i];
-    double vx, vy;
-    fit_event<0>(c, e, seq, vx, vy);
+    fit_event_fast<FR>(c, e, seq, s_tk + threadIdx.x, vx, vy);
     fit_store(c, e, vx, vy);
 }
 
+
 // ---------------------------------------------------------------------------
-// Candidate-cell bitmap for pooling chunk `chunk_idx` into ring buffer b: bit q
-// set if q is touched in the chunk, or its snapshot flow is valid and within the
-// kill time of some event of the chunk (a superset of every cell that can
-// contribute to any event of the chunk).  One wave ballot per 64 cells.
-__global__ void k_bitmap(Ctx c, int chunk_idx, uint32_t seq, int b) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool act = false;
-    if (q < c.WH) {
-        act = c.ptouch[q].seq == seq;
-        if (!act) {
-            const int64_t ft = c.ftime[q];
-            const int64_t lo = (int64_t)c.ctmin[chunk_idx] - (int64_t)kKillUs;
-            const int64_t hi = (int64_t)c.ctmax[chunk_idx] + (int64_t)kKillUs;
-            act = ft >= 0 && ft > lo && ft < hi;
+// Wave-cooperative fit of one event (any fRad, every lookup complete): the
+// lanes resolve the stamps of the union of the 9 candidate windows into LDS
+// (these lookups are the latency: pixels with many in-chunk events need a run
+// search) and reduce the integer window scores and normal-matrix sums; lane 0
+// then runs the order-sensitive (A2*At)*Y accumulation from LDS.  Arithmetic
+// is that of fit_event, so results are bitwise those of the per-thread path.
+constexpr int kFitWaveCap = 1024;  // union-window cells staged per wave
+constexpr int kFitWaveBlocks = 2048;  // fixed grid of k_fit_wave (4 waves per block)
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t, uint8_t *s_v, int lane) {
+    const int fr = c.fr, side = 2 * fr + 1, np = side * side, US = 4 * fr + 1, nU = US * US;
+    const int W = c.W, H = c.H;
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t te = c.t[e];
+    if (nU > kFitWaveCap) {  // very large filters: per-thread path on lane 0
+        if (lane == 0) {
+            double vx, vy;
+            fit_event_generic(c, e, seq, vx, vy);
+            fit_store(c, e, vx, vy);
+        }
+        return;
+    }
+    bool wok[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * fr, cj = ey + (w % 3 - 1) * fr;
+        wok[w] = ci - fr >= 0 && ci + fr <= W - 1 && cj - fr >= 0 && cj + fr <= H - 1;
+        any |= wok[w];
+    }
+    if (!any) {
+        if (lane == 0) fit_store(c, e, 0.0, 0.0);
+        return;
+    }
+    // ---- stage the union window and score the 9 windows (vFlow.cpp:870-912)
+    int64_t score[9];
+#pragma unroll
+    for (int w = 0; w < 9; ++w) score[w] = 0;
+    for (int idx = lane; idx < nU; idx += 64) {
+        const int du = idx / US - 2 * fr, dv = idx % US - 2 * fr;
+        const int u = ex + du, v = ey + dv;
+        const bool ins = u >= 0 && u < W && v >= 0 && v < H;
+        int64_t st = -1;
+        if (ins && u >= c.X0 && u < c.XR1) st = sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq);
+        const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+        s_t[idx] = tk;
+        s_v[idx] = st >= 0 ? 1 : 0;
+        if (ins) {
+            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                const int ou = (w / 3 - 1) * fr, ov = (w % 3 - 1) * fr;
+                if (wok[w] && du - ou <= fr && ou - du <= fr && dv - ov <= fr && ov - dv <= fr) score[w] += d;
+            }
         }
     }
-    const uint64_t bal = __ballot(act);
-    if ((threadIdx.x & 63) == 0 && (q >> 6) < c.nwords) {
-        c.bm_ring[(int64_t)b * c.nwords + (q >> 6)] = bal;
-        c.wc_ring[(int64_t)b * c.nwords + (q >> 6)] = (uint32_t)__popcll(bal);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int64_t sw = wave_sum_i64(score[w]);
+        if (wok[w] && sw < best) { best = sw; bw = w; }
+    }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) {
+        if (lane == 0) fit_store(c, e, 0.0, 0.0);
+        return;
+    }
+    // ---- the winning window, cx-major (vFlow.cpp:923-930)
+    const int bi = ex + (bw / 3 - 1) * fr, bj = ey + (bw % 3 - 1) * fr;
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+        const int cx = bi + k / side - fr, cy = bj + k % side - fr;
+        const int idx = (cx - ex + 2 * fr) * US + (cy - ey + 2 * fr);
+        const bool vk = s_v[idx] != 0;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = s_t[idx];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
+    for (int k = lane; k < np; k += 64) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    sxx = wave_sum_i64(sxx); sxy = wave_sum_i64(sxy); sx = wave_sum_i64(sx);
+    syy = wave_sum_i64(syy); sy = wave_sum_i64(sy);
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    int inliers = 0;
+    double dtdx = 0.0, dtdy = 0.0;
+    if (!(DET < 1)) {
+        DET = 1.0 / DET;  // vFlow.cpp:1327-1336
+        const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+        const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+        const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+        const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+        const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+        const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+        const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+        const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+        const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+        const bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+        const double cz = (double)te * kTsToSec;
+        double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+        if (lane == 0) {  // order-sensitive: one lane, stamps from LDS
+            for (int k = 0; k < np; ++k) {
+                int64_t Xi, Yi; uint32_t T;
+                cell(k, Xi, Yi, T);
+                const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+                const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+                double m0, m1, m2;
+                if (gemm) {
+                    m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+                    m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+                    m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+                } else {
+                    m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+                    m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+                    m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+                }
+                if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+                else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+            }
+            if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+        }
+        r0 = __shfl(r0, 0, 64);
+        r1 = __shfl(r1, 0, 64);
+        const double dtdp = sqrt(r0 * r0 + r1 * r1);
+        const double ccx = (double)ex, ccy = (double)ey;
+        int inl = 0;
+        for (int k = lane; k < np; k += 64) {
+            int64_t Xi, Yi; uint32_t T;
+            cell(k, Xi, Yi, T);
+            const double Tk = (double)T;
+            const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+            const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+            const double actualdt = yt - cz;
+            if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inl;
+        }
+        inliers = (int)wave_sum_i64(inl);
+        const double speed = 1.0 / dtdp;
+        const double angle = atan2(r0, r1);
+        dtdx = speed * cos(angle);
+        dtdy = speed * sin(angle);
+    }
+    if (lane == 0) {
+        double vx = 0.0, vy = 0.0;
+        if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
+        fit_store(c, e, vx, vy);
     }
 }
 
-// Exclusive prefix of buffer b's per-word popcounts (single workgroup of 1024):
-// per-thread serial sums, wave scans, one LDS pass over the 16 wave totals.
-__global__ __launch_bounds__(1024) void k_scan(Ctx c, int b) {
-    __shared__ uint32_t wsum[16];
-    const uint32_t *wc = c.wc_ring + (int64_t)b * c.nwords;
-    uint32_t *wo = c.wo_ring + (int64_t)b * (c.nwords + 1);
-    const int64_t nw = c.nwords;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t per = (nw + 1023) / 1024;
-    const int64_t w0 = tid * per, w1 = w0 + per < nw ? w0 + per : nw;
-    uint32_t sum = 0;
-    for (int64_t w = w0; w < w1; ++w) sum += wc[w];
-    uint32_t incl = sum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += v;
+// Waves loop over the events list[0 .. count) (every event of a chunk, for
+// filters without a compile-time fast path).  The grid is fixed; every wave
+// reaches the loop end.
+__global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int32_t *list, int count) {
+    __shared__ uint32_t s_t[4][kFitWaveCap];
+    __shared__ uint8_t s_v[4][kFitWaveCap];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = count;
+    const int stride = (int)gridDim.x * 4;
+    for (int i = (int)blockIdx.x * 4 + wv; i < n; i += stride) {
+        fit_wave_event(c, list[i], seq, s_t[wv], s_v[wv], lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int k = 0; k < wv; ++k) base += wsum[k];
-    uint32_t run = base + incl - sum;
-    for (int64_t w = w0; w < w1; ++w) {
-        wo[w] = run;
-        run += wc[w];
-    }
-    if (tid == 1023) wo[nw] = run;
+}
+
+// ---------------------------------------------------------------------------
+// Cross-lane exchange with the partner lane l ^ (1 << S): DPP quad
+// permutations for S = 0, 1, ds_swizzle (bitmask mode, 32-lane groups) for
+// S = 2..4, ds_bpermute for S = 5.
+template <int S>
+__device__ __forceinline__ int xch32(int v) {
+    if constexpr (S == 0) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    else if constexpr (S == 1) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    else if constexpr (S == 2) return __builtin_amdgcn_ds_swizzle(v, 0x101F);
+    else if constexpr (S == 3) return __builtin_amdgcn_ds_swizzle(v, 0x201F);
+    else if constexpr (S == 4) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
+    else return __shfl_xor(v, 32, 64);
+}
+template <int S>
+__device__ __forceinline__ double xch(double v) {
+    return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
+}
+
+constexpr int kBlkCells = 1024;  // cells per candidate-count block (256 threads x 4)
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += (uint32_t)xch32<0>((int)v);
+    v += (uint32_t)xch32<1>((int)v);
+    v += (uint32_t)xch32<2>((int)v);
+    v += (uint32_t)xch32<3>((int)v);
+    v += (uint32_t)xch32<4>((int)v);
+    v += (uint32_t)xch32<5>((int)v);
+    return v;
 }
 
 // Candidate index (in buffer b) of the first candidate with cell index >= L.
@@ -685,16 +949,10 @@ __device__ __forceinline__ uint32_t cand_index(const Ctx &c, int b, int64_t L) {
     return k;
 }
 
-// Materialise the candidate records of the chunk into buffer b (thread per cell).
-__global__ void k_fill(Ctx c, uint32_t seq, int b) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= c.WH) return;
-    const uint64_t bits = c.bm_ring[(int64_t)b * c.nwords + (q >> 6)];
-    const int r = (int)(q & 63);
-    if (!((bits >> r) & 1)) return;
-    const uint32_t k = c.wo_ring[(int64_t)b * (c.nwords + 1) + (q >> 6)] +
-                       (uint32_t)__popcll(bits & ((1ull << r) - 1));
-    const PoolTouch pt = c.ptouch[q];
+// Candidate record k of buffer b <- cell q: snapshot flow and, if the cell is
+// touched in the chunk (pt.seq == seq), its first in-chunk flow and run bounds.
+__device__ __forceinline__ void fill_cell(const Ctx &c, uint32_t seq, int b, int64_t q, uint32_t k,
+                                          const PoolTouch &pt, int2 run) {
     const FlowCell snap = c.fsnap[q];
     CandHdr hd;
     CandVal v;
@@ -704,7 +962,6 @@ __global__ void k_fill(Ctx c, uint32_t seq, int b) {
     if (pt.seq == seq) {
         const int e1 = (int)(pt.e1m & kSeqMask);
         const FlowCell f1 = c.evf[e1];
-        const int2 run = c.ptpos[q];
         hd.e1 = e1;
         hd.lin |= (pt.e1m & 0x80000000u ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
         hd.t1 = f1.t;
@@ -721,6 +978,113 @@ __global__ void k_fill(Ctx c, uint32_t seq, int b) {
     c.val_ring[kb] = v;
 }
 
+// The pooling sweep's candidate chain, one launch per pooling chunk ch:
+//   cell blocks (one cell per thread; candidate counts are kept per group of
+//   kBlkCells = 4 blocks):
+//     - fill: materialise chunk ch's candidate records into ring buffer
+//       ch % NB (its bitmap and per-group counts come from launch ch-1; each
+//       block sums the counts of the groups before it, so there is no scan
+//       pass) and record the candidate offset of each bitmap word;
+//     - flow snapshot <- the last chunk-ch event at each cell ch touched;
+//     - bitmap of chunk ch+1 into buffer (ch+1) % NB: bit q set if q is
+//       touched in ch+1 or its (new) snapshot flow is valid and within the kill
+//       time of some event of ch+1 — a superset of every cell that can
+//       contribute to an event of ch+1 — and the group's candidate count
+//       (atomic adds of the 4 block counts; the group counts of buffer
+//       (ch+2) % NB are cleared here for launch ch+1);
+//   event blocks: first in-chunk event and run bounds of every cell touched by
+//   chunk ch+2 (touch state is triple-buffered by chunk).
+// Launches ch = -2 and -1 prime the chain (touch of chunks 0 and 1, bitmap of 0).
+__global__ __launch_bounds__(256) void k_chain(Ctx c, int ch, int nch, uint32_t seq0) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ncb = c.nblk * (kBlkCells / 256);  // cell blocks
+    if ((int)blockIdx.x >= ncb) {  // ---- event role: touch chunk ch+2
+        const int tc = ch + 2;
+        if (tc < 0 || tc >= nch) return;
+        const int n0 = tc * c.C2, n1 = min(n0 + c.C2, c.n);
+        const int e = n0 + ((int)blockIdx.x - ncb) * 256 + tid;
+        if (e >= n1) return;
+        const int64_t so = (int64_t)(tc % 3) * c.WH;
+        const uint32_t q = c.pix[e];
+        const int nx = c.next[e];
+        if (c.prev[e] < n0) {
+            c.ptouch[so + q] = PoolTouch{seq0 + (uint32_t)tc, (uint32_t)e | (nx < n1 ? 0x80000000u : 0u)};
+            c.ptpos[so + q].x = c.pos[e];
+        }
+        if (nx >= n1) c.ptpos[so + q].y = c.pos[e];
+        return;
+    }
+    // ---- cell role
+    __shared__ uint32_t s_red[4], s_bef[4], s_off[5];
+    const bool fill = ch >= 0 && ch < nch;
+    const bool next = ch + 1 >= 0 && ch + 1 < nch;
+    const int grp = (int)blockIdx.x >> 2, sub = (int)blockIdx.x & 3;  // group of 1024 cells, block within it
+    const int64_t q = (int64_t)blockIdx.x * 256 + tid;
+    const int64_t w = q >> 6;  // this wave's bitmap word
+    const int b = fill ? ch % c.NB : 0, bn = next ? (ch + 1) % c.NB : 0;
+    const uint32_t seq = seq0 + (uint32_t)ch, seqn = seq + 1u;
+    if (tid == 0 && sub == 0) c.blk_ring[(int64_t)((ch + 2 + c.NB) % c.NB) * c.nblk + grp] = 0;
+    uint64_t bits = 0;
+    uint32_t woff = 0;
+    if (fill) {
+        const uint32_t *blk = c.blk_ring + (int64_t)b * c.nblk;
+        uint32_t before = 0;
+        for (int i = tid; i < grp; i += 256) before += blk[i];
+        before = wave_sum_u32(before);
+        // words of the group before this block's, then this block's 4 words
+        const int64_t gw0 = (int64_t)grp * (kBlkCells / 64);
+        uint32_t pre = 0;
+        if (lane < 4 * sub) pre = gw0 + lane < c.nwords ? (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + gw0 + lane]) : 0u;
+        pre = wave_sum_u32(pre);
+        bits = w < c.nwords ? c.bm_ring[(int64_t)b * c.nwords + w] : 0ull;
+        if (lane == 0) { s_red[wv] = (uint32_t)__popcll(bits); s_bef[wv] = before; }
+        __syncthreads();
+        if (tid == 0) {
+            // groups before: the 4 waves' partial sums; words before in the group:
+            // every wave computed the same `pre`
+            uint32_t run = s_bef[0] + s_bef[1] + s_bef[2] + s_bef[3] + pre;
+            for (int i = 0; i < 4; ++i) { s_off[i] = run; run += s_red[i]; }
+            s_off[4] = run;
+        }
+        __syncthreads();
+        woff = s_off[wv];
+        uint32_t *wo = c.wo_ring + (int64_t)b * (c.nwords + 1);
+        if (lane == 0 && w < c.nwords) wo[w] = woff;
+        if (tid == 0 && (int64_t)blockIdx.x == (c.WH + 255) / 256 - 1) wo[c.nwords] = s_off[4];
+    }
+    bool act = false;
+    if (q < c.WH) {
+        int64_t ft = c.ftime[q];
+        if (fill) {
+            const int64_t so = (int64_t)(ch % 3) * c.WH;
+            const PoolTouch pt = c.ptouch[so + q];
+            const bool touched = pt.seq == seq;
+            int2 run = make_int2(0, 0);
+            if (touched) run = c.ptpos[so + q];
+            if ((bits >> lane) & 1)
+                fill_cell(c, seq, b, q, woff + (uint32_t)__popcll(bits & ((1ull << lane) - 1)), pt, run);
+            if (touched) {  // snapshot <- last event of the chunk at q (after fill read the old one)
+                const FlowCell f = c.evf[c.P[run.y]];
+                c.fsnap[q] = f;
+                ft = f.L > 0 ? (int64_t)f.t : -1;
+                c.ftime[q] = ft;
+            }
+        }
+        if (next) {
+            const int64_t lo = (int64_t)c.ctmin[ch + 1] - (int64_t)kKillUs;
+            const int64_t hi = (int64_t)c.ctmax[ch + 1] + (int64_t)kKillUs;
+            act = c.ptouch[(int64_t)((ch + 1) % 3) * c.WH + q].seq == seqn || (ft >= 0 && ft > lo && ft < hi);
+        }
+    }
+    if (next) {
+        const uint64_t bal = __ballot(act);
+        if (lane == 0) {
+            if (w < c.nwords) c.bm_ring[(int64_t)bn * c.nwords + w] = bal;
+            if (bal) atomicAdd(&c.blk_ring[(int64_t)bn * c.nblk + grp], (uint32_t)__popcll(bal));
+        }
+    }
+}
+
 // Last event with id <= e over a candidate's in-chunk run P[lo..hi] (P[lo] <= e).
 __device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, int e) {
     if (c.P[hi] <= e) return hi;
@@ -732,35 +1096,45 @@ __device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, i
     return lo;
 }
 
-// Butterfly sums over the 64 lanes: quad xor-1, xor-2, row half-mirror and
-// row mirror by DPP, then xor-16 / xor-32 by permute.  Every lane ends with the
-// same value (each step adds a pair in both orders), so the result does not
-// depend on which lane reads it.
-template <int CTRL>
-__device__ __forceinline__ int dpp32(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+// Transposed butterfly over P = 2^LP slots per lane: at step S each lane keeps
+// the slots whose bit S equals its lane bit S and adds the partner's copy, so
+// step S moves P / 2^(S+1) values; after LP steps the lane holds one slot, and
+// the remaining steps are a plain butterfly.  On return v[0] is the wave total
+// of slot (lane & (P - 1)).  Every slot is combined by the same tree (a + b is
+// commutative), so slots with bitwise-equal lane partials get bitwise-equal
+// totals.
+template <int S, int LP, int N>
+__device__ __forceinline__ void tsum_step(double (&v)[N], int lane) {
+    if constexpr (S < 6) {
+        if constexpr (S < LP) {
+            constexpr int half = N >> (S + 1);
+            const bool hi = (lane >> S) & 1;
+#pragma unroll
+            for (int p = 0; p < half; ++p) {
+                const double lo = v[2 * p], up = v[2 * p + 1];
+                const double send = hi ? lo : up, keep = hi ? up : lo;
+                v[p] = keep + xch<S>(send);
+            }
+        } else {
+            v[0] = v[0] + xch<S>(v[0]);
+        }
+        tsum_step<S + 1, LP, N>(v, lane);
+    }
 }
-template <int CTRL>
-__device__ __forceinline__ double dpp64(double v) {
-    const int lo = dpp32<CTRL>(__double2loint(v)), hi = dpp32<CTRL>(__double2hiint(v));
-    return __hiloint2double(hi, lo);
+template <int LP, int N>
+__device__ __forceinline__ void tsum(double (&v)[N], int lane) {
+    static_assert(N == (1 << LP), "slot count");
+    tsum_step<0, LP, N>(v, lane);
 }
-__device__ __forceinline__ double wave_sum(double v) {
-    v += dpp64<0xB1>(v);   // quad_perm [1,0,3,2]
-    v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
-    v += dpp64<0x141>(v);  // row_half_mirror
-    v += dpp64<0x140>(v);  // row_mirror
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
-}
-__device__ __forceinline__ int wave_sum_i(int v) {
-    v += dpp32<0xB1>(v);
-    v += dpp32<0x4E>(v);
-    v += dpp32<0x141>(v);
-    v += dpp32<0x140>(v);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
+
+// Max over the 64 lanes (exact).
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, xch<0>(v));
+    v = fmax(v, xch<1>(v));
+    v = fmax(v, xch<2>(v));
+    v = fmax(v, xch<3>(v));
+    v = fmax(v, xch<4>(v));
+    v = fmax(v, xch<5>(v));
     return v;
 }
 
@@ -782,7 +1156,7 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 template <int K>
 __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     __shared__ int s_pre[4][130];       // per wave: prefix of candidate counts over rows
-    __shared__ int s_a[4][128];         // per wave: first candidate of each row
+    __shared__ int s_skip[4][128];      // per wave: candidate index - flattened index, per row
     __shared__ uint2 s_con[4][kPoolCap];  // per wave: contributors {ref, kind | k0 << 8}
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -818,7 +1192,6 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
                 a = (int)cand_index(c, buf, l0);
                 cnt = (int)cand_index(c, buf, l1 + 1) - a;
             }
-            s_a[wv][r] = a;
         }
         int incl = cnt;  // inclusive wave scan
 #pragma unroll
@@ -826,7 +1199,10 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
             const int v = __shfl_up(incl, off, 64);
             if (lane >= off) incl += v;
         }
-        if (r < nrows) s_pre[wv][r + 1] = carry + incl;
+        if (r < nrows) {
+            s_pre[wv][r + 1] = carry + incl;
+            s_skip[wv][r] = a - (carry + incl - cnt);
+        }
         carry += __shfl(incl, 63, 64);
     }
     if (lane == 0) s_pre[wv][0] = 0;
@@ -841,22 +1217,37 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     auto collect = [&](int pass) -> int {
         const int rank_lo = pass * kPoolCap, rank_hi = rank_lo + kPoolCap;
         int ncon = 0;
-        int r = 0;  // row of the next candidate this lane will locate
-        auto locate = [&](int f, int &row, int &k) {
-            while (f >= s_pre[wv][r + 1]) ++r;
+        // Rows of the flattened window [fw, fw + 64): lane f's row is r0 plus
+        // the number of row ends s_pre[r0 + d + 1] <= f.  Each lane loads one
+        // upcoming row end and the wave walks them by readlane (uniform loop),
+        // which also advances r0 to the row of fw + 64.
+        int r0 = 0;
+        auto locate = [&](int fw, int f, int &row, int &k) {
+            int r = r0;
+            for (int base = r0;;) {
+                const int myb = base + lane < nrows ? s_pre[wv][base + lane + 1] : INT_MAX;
+                int d = 0;
+                for (; d < 64; ++d) {
+                    const int bnd = __builtin_amdgcn_readlane(myb, d);
+                    if (bnd > fw + 64) break;
+                    r += f >= bnd ? 1 : 0;
+                }
+                base += d;
+                if (d < 64) { r0 = base; break; }
+            }
             row = r;
-            k = s_a[wv][r] + (f - s_pre[wv][r]);
+            k = f + s_skip[wv][r < nrows ? r : nrows - 1];
         };
         // software pipeline: the header of step s+1 is in flight while step s
         // is resolved
         int rc = 0, kc = 0;
         CandHdr hc{};
-        if (lane < total) { locate(lane, rc, kc); hc = chdr[kc]; }
+        if (total > 0) { locate(0, lane, rc, kc); if (lane < total) hc = chdr[kc]; }
         for (int f0 = 0; f0 < total; f0 += 64) {
             const int f = f0 + lane, fn = f + 64;
             int rn = 0, kn = 0;
             CandHdr hn{};
-            if (fn < total) { locate(fn, rn, kn); hn = chdr[kn]; }
+            if (f0 + 64 < total) { locate(f0 + 64, fn, rn, kn); if (fn < total) hn = chdr[kn]; }
             bool con = false;
             uint32_t ref = 0, meta = 0;
             if (f < total) {
@@ -901,8 +1292,8 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
         else if (kind == 1) { const CandVal &v = cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
         else { const FlowCell fe = c.evf[en.x]; L = fe.L; Lc = fe.Lc; Ls = fe.Ls; }
     };
-    // ---- phase B1: mean length per scale; lane l takes a contiguous share of
-    // each staged batch
+    // ---- phase B1: length sum and count per scale; lane l takes a contiguous
+    // share of each staged batch
     double sL[K];
     int cntk[K];
 #pragma unroll
@@ -926,19 +1317,31 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
                 if (kk >= k0) { sL[kk] += L; cntk[kk] += 1; }
         }
     }
-    // first strict max of the mean length over scales (vFlow.cpp:1023-1059);
-    // every lane holds the same butterfly sums, so every lane finds the same k*
-    double maxv = 0.0;
-    int mi = 0, cnt_mi = 0;
+    // wave totals: slot 2k = length sum of scale k, slot 2k+1 = its count
+    constexpr int LP = K <= 4 ? 3 : (K <= 8 ? 4 : 5);
+    double slot[1 << LP];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double sk = wave_sum(sL[k]);
-        const int ck = wave_sum_i(cntk[k]);
-        const double mean = ck > 0 ? sk / (double)ck : 0.0;
-        if (mean > maxv) { maxv = mean; mi = k; cnt_mi = ck; }
+    for (int q = 0; q < (1 << LP); ++q) slot[q] = 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { slot[2 * k] = sL[k]; slot[2 * k + 1] = (double)cntk[k]; }
+    tsum<LP>(slot, lane);
+    // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
+    // lane 2k (mod 2^LP) holds scale k's mean; the winner is the lowest k
+    // whose mean equals the maximum, if the maximum is > 0
+    const double mine = slot[0], partner = xch<0>(slot[0]);
+    const int sl = lane & ((1 << LP) - 1);
+    const bool is_len = !(sl & 1) && (sl >> 1) < K;
+    const double mean = is_len && partner > 0 ? mine / partner : 0.0;
+    const double maxv = wave_max(mean);
+    int mi = 0, cnt_mi = 0;
+    if (maxv > 0) {
+        const uint64_t hit = __ballot(is_len && mean == maxv);
+        const int lw = __builtin_ctzll(hit);
+        mi = (lw & ((1 << LP) - 1)) >> 1;
+        cnt_mi = (int)__shfl(partner, lw, 64);
     }
     // ---- phase B2: mean vector of the winning scale (vFlow.cpp:1067-1075)
-    double sX = 0.0, sY = 0.0;
+    double sXY[2] = {0.0, 0.0};
     if (maxv > 0) {
         for (int pass = 0; pass < npass; ++pass) {
             if (npass > 1) {  // re-stage batch `pass` (a single batch is still in LDS)
@@ -952,14 +1355,14 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
                 if ((int)(en.y >> 8) <= mi) {
                     double L, Lc, Ls;
                     value_of(en, L, Lc, Ls);
-                    sX += Lc;
-                    sY += Ls;
+                    sXY[0] += Lc;
+                    sXY[1] += Ls;
                 }
             }
         }
     }
-    sX = wave_sum(sX);
-    sY = wave_sum(sY);
+    tsum<1>(sXY, lane);  // even lanes: sum of Lc, odd lanes: sum of Ls
+    const double sX = sXY[0], sY = xch<0>(sXY[0]);
     if (lane == 0) {
         double gx, gy;
         int sc;
@@ -1045,10 +1448,11 @@ struct farms_handle {
     FlowCell *fsnap = nullptr;
     PoolTouch *ptouch = nullptr;
     int2 *ptpos = nullptr;
-    // ring of per-chunk candidate buffers (NB = 2 x pool_batch)
-    int pool_batch = 8, NB = 16;
+    // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1)
+    int pool_batch = 16, NB = 33;
     uint64_t *bm_ring = nullptr;
-    uint32_t *wc_ring = nullptr, *wo_ring = nullptr;
+    uint32_t *blk_ring = nullptr, *wo_ring = nullptr;
+    int nblk = 0;
     CandHdr *hdr_ring = nullptr;
     CandVal *val_ring = nullptr;
     int64_t nwords = 0;
@@ -1071,8 +1475,7 @@ struct farms_handle {
     uint32_t *ctmin = nullptr, *ctmax = nullptr;
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
-    int *err = nullptr, *defer_count = nullptr;
-    int32_t *defer = nullptr;
+    int *err = nullptr;
     unsigned long long *counters = nullptr;
     bool profiling = false;
     hipEvent_t ev[8] = {};
@@ -1098,7 +1501,7 @@ void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->pos); dfree(h->prev); dfree(h->next);
     dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
-    dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->defer); dfree(h->ctmin); dfree(h->ctmax);
+    dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
     h->cub_bytes = 0;
@@ -1123,7 +1526,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
         (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
-        (rc = dalloc(&h->defer, std::min<int64_t>(cap, h->fit_chunk))) || (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
+        (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
         (rc = dalloc(&h->ctmax, nch))) {
         free_workspace(h);
         return rc;
@@ -1148,7 +1551,7 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipMemsetAsync(h->tpos, 0, sizeof(int2) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->ptouch, 0, sizeof(PoolTouch) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->ptouch, 0, sizeof(PoolTouch) * 3 * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     return FARMS_OK;
@@ -1179,7 +1582,7 @@ void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t 
     case 1: hipLaunchKernelGGL(k_fit<1>, g, b, 0, s, c, c0, c1, seq); break;
     case 2: hipLaunchKernelGGL(k_fit<2>, g, b, 0, s, c, c0, c1, seq); break;
     case 3: hipLaunchKernelGGL(k_fit<3>, g, b, 0, s, c, c0, c1, seq); break;
-    default: hipLaunchKernelGGL(k_fit<0>, g, b, 0, s, c, c0, c1, seq); break;
+    default: break;  // k_fit_wave
     }
 }
 
@@ -1217,7 +1620,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.cells = h->cells; c.tpos = h->tpos; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.ptouch = h->ptouch; c.ptpos = h->ptpos;
-    c.bm_ring = h->bm_ring; c.wc_ring = h->wc_ring; c.wo_ring = h->wo_ring;
+    c.bm_ring = h->bm_ring; c.blk_ring = h->blk_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
@@ -1226,8 +1629,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
     c.counters = h->counters;
     c.dbg_tc = h->profiling ? h->dbg_tc : nullptr;
-    c.defer = h->defer;
-    c.defer_count = h->defer_count;
 
     const bool prof = h->profiling;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
@@ -1273,53 +1674,67 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
 
-    // ---- sweep 1 (stream F): local plane fits, chunk after chunk
-    int fit_launches = 0;
-    for (int c0 = 0; c0 < n; c0 += h->fit_chunk) {
-        const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->fit_chunk, n);
-        const uint32_t seq = ++h->seq;
-        const dim3 g(ceil_div(c1 - c0, 256)), b(256);
-        hipLaunchKernelGGL(k_touch, g, b, 0, s, c, c0, c1, seq);
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches], s));
-        HIPCHK(hipMemsetAsync(h->defer_count, 0, sizeof(int), s));
-        launch_fit(c, h->fr, c0, c1, seq, s);
-        if (h->fr >= 1 && h->fr <= 3)
-            hipLaunchKernelGGL(k_fit_generic, g, b, 0, s, c, seq);
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * fit_launches + 1], s));
-        HIPCHK(hipEventRecord(ev_fit(fit_launches), s));
-        hipLaunchKernelGGL(k_sae_update, g, b, 0, s, c, c0, c1);
-        ++fit_launches;
-    }
-    HIPCHK(hipGetLastError());
-    if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
-
-    // ---- sweep 2: candidate lists on stream C (a serial chain over chunks,
-    // each chunk into ring buffer ch % NB), pooling kernels on stream P, one
-    // launch per super-chunk of B chunks.  Pooling of a chunk reads only its
-    // candidate buffer, the per-event flows and P, so it overlaps the chain of
-    // later chunks and the fit sweep.
-    hipStream_t sc = h->s_chain, sp = h->s_pool;
+    // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
+    // pooling chain as soon as the first fits are done:
+    //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
+    //     or k_fit_wave for filters without a compile-time fast path);
+    //   stream C: the candidate chain, one k_chain per pooling chunk, each
+    //     chunk's records into ring buffer ch % NB (NB = 2B + 1);
+    //   stream P: one k_pool per super-chunk of B pooling chunks.
+    // Pooling of a chunk reads only its candidate buffer, the per-event flows
+    // and P, so it overlaps the chain of later chunks and the fit sweep.
+    // FARMS_SERIALIZE=1 puts everything on one stream (profiling aid: kernel
+    // durations without overlap).
+    const char *ser = getenv("FARMS_SERIALIZE");
+    const bool serial = ser && ser[0] == '1';
+    hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
     pool_launcher pl = pool_for(h->K);
-    const int bm_blocks = ceil_div(h->nwords * 64, 256);
-    const int cell_blocks = ceil_div(h->WH, 256);
+    const bool fast_fit = h->fr >= 1 && h->fr <= 3;
+    int fit_launches = 0;
+    auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
+    auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F
+        const int c0 = f * h->fit_chunk, c1 = fit_chunk_end(f), p0 = f > 0 ? (f - 1) * h->fit_chunk : 0;
+        const uint32_t seq = ++h->seq;
+        hipLaunchKernelGGL(k_fit_prep, dim3(ceil_div(std::max(c1 - c0, c0 - p0), 256)), dim3(256), 0, s, c, p0, c0,
+                           c1, seq);
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * f], s));
+        if (fast_fit) {
+            launch_fit(c, h->fr, c0, c1, seq, s);
+        } else {  // no per-thread fast path for this filter: every event wave-cooperative
+            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, c, seq, h->Q + c0, c1 - c0);
+        }
+        if (prof) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
+        HIPCHK(hipEventRecord(ev_fit(f), s));
+        ++fit_launches;
+        if (f == n_fit_chunks - 1) {  // SAE snapshot of the last chunk (streaming state)
+            hipLaunchKernelGGL(k_fit_prep, dim3(ceil_div(n - c0, 256)), dim3(256), 0, s, c, c0, n, n, 0u);
+            if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
+        }
+        return FARMS_OK;
+    };
+    const uint32_t pseq0 = h->seq + 1;  // pooling chunk ch has sequence pseq0 + ch
+    h->seq += (uint32_t)n_pool_chunks + 2;
+    const int chain_grid = h->nblk * (kBlkCells / 256) + ceil_div(h->pool_chunk, 256);
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
-    int fit_waited = -1;
+    if (n_pool_chunks > 0) {  // prime: touch chunks 0 and 1, bitmap of chunk 0
+        hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, -2, n_pool_chunks, pseq0);
+        hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, -1, n_pool_chunks, pseq0);
+    }
+    int fit_enqueued = 0, fit_waited = -1;
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
+        // keep the fit sweep one super-chunk ahead of the chain
+        const int need = std::min(n_fit_chunks, ceil_div(std::min<int64_t>((int64_t)(ch1 + B) * h->pool_chunk, n),
+                                                         h->fit_chunk));
+        while (fit_enqueued < need) {
+            int rc = enqueue_fit(fit_enqueued++);
+            if (rc) return rc;
+        }
         if (S >= 2) HIPCHK(hipStreamWaitEvent(sc, ev_pool(S - 2), 0));  // ring buffers of S-2 are free
         for (int ch = ch0; ch < ch1; ++ch) {
-            const int c0 = ch * h->pool_chunk;
-            const int c1 = (int)std::min<int64_t>((int64_t)c0 + h->pool_chunk, n);
-            const int f = c0 / h->fit_chunk;  // fit chunks are whole pooling chunks
+            const int f = (int)((int64_t)ch * h->pool_chunk / h->fit_chunk);  // fit chunks are whole pooling chunks
             if (f > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(f), 0)); fit_waited = f; }
-            const uint32_t seq = ++h->seq;
-            const int buf = ch % h->NB;
-            const dim3 g(ceil_div(c1 - c0, 256)), b(256);
-            hipLaunchKernelGGL(k_touch_pool, g, b, 0, sc, c, c0, c1, seq);
-            hipLaunchKernelGGL(k_bitmap, dim3(bm_blocks), dim3(256), 0, sc, c, ch, seq, buf);
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, sc, c, buf);
-            hipLaunchKernelGGL(k_fill, dim3(cell_blocks), dim3(256), 0, sc, c, seq, buf);
-            hipLaunchKernelGGL(k_flow_update, g, b, 0, sc, c, c0, c1);
+            hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, ch, n_pool_chunks, pseq0);
         }
         HIPCHK(hipEventRecord(ev_cand(S), sc));
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
@@ -1329,6 +1744,11 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
         HIPCHK(hipEventRecord(ev_pool(S), sp));
     }
+    while (fit_enqueued < n_fit_chunks) {
+        int rc = enqueue_fit(fit_enqueued++);
+        if (rc) return rc;
+    }
+    HIPCHK(hipGetLastError());
     const int pool_launches = n_super;
     HIPCHK(hipGetLastError());
     // join: stream F waits for the last chain step and the last pooling launch
@@ -1432,8 +1852,9 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
     if (prm->pool_batch > 0) h->pool_batch = prm->pool_batch;
-    h->NB = 2 * h->pool_batch;
+    h->NB = 2 * h->pool_batch + 1;
     h->nwords = (h->WH + 63) / 64;
+    h->nblk = (int)((h->WH + 1023) / 1024);
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     {
@@ -1442,17 +1863,21 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     }
     int rc = FARMS_OK;
     auto bail = [&](int code) { farms_destroy(h); return code; };
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->s_chain, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->s_pool, hipStreamNonBlocking) != hipSuccess)
+    // the fit sweep and the candidate chain are the latency-critical dependency
+    // path: high priority; the bulk pooling launches fill the remaining CUs
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->tpos, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ptouch, h->WH)) || (rc = dalloc(&h->ptpos, h->WH)) ||
-        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || (rc = dalloc(&h->wc_ring, h->nwords * h->NB)) ||
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ptouch, 3 * h->WH)) || (rc = dalloc(&h->ptpos, 3 * h->WH)) ||
+        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || (rc = dalloc(&h->blk_ring, (int64_t)h->nblk * h->NB)) ||
         (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->WH * h->NB)) ||
-        (rc = dalloc(&h->val_ring, h->WH * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->defer_count, 1)) || (rc = dalloc(&h->counters, 8)))
+        (rc = dalloc(&h->val_ring, h->WH * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
@@ -1466,8 +1891,8 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     free_workspace(h);
     dfree(h->cells); dfree(h->tpos); dfree(h->ftime); dfree(h->fsnap);
-    dfree(h->ptouch); dfree(h->ptpos); dfree(h->bm_ring); dfree(h->wc_ring); dfree(h->wo_ring);
-    dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->defer_count); dfree(h->counters);
+    dfree(h->ptouch); dfree(h->ptpos); dfree(h->bm_ring); dfree(h->blk_ring); dfree(h->wo_ring);
+    dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);

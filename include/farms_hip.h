@@ -56,7 +56,7 @@ typedef struct {
      * sensor), owned records are bitwise those of a whole-sensor run. */
     int32_t region_x0, region_width;
     int32_t own_x0, own_x1;
-    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (8) */
+    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (16) */
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA

@@ -13,7 +13,7 @@ case $SET in
   tcc) CTRS="TCC_HIT_sum TCC_MISS_sum";;
   ta)  CTRS="TA_BUSY_avr TA_TA_BUSY_sum SQ_INSTS_SMEM SQ_INSTS_SALU";;
 esac
-timeout -k 10 500 rocprofv3 --pmc $CTRS --kernel-include-regex 'k_pool|k_fit' -d gpurun_out/pmc_$SET -o pmc \
-   --output-format csv -- python3 tools/sweep.py --events $EV --pool 32768 --fit 262144 --reps 1 \
+timeout -k 10 500 rocprofv3 --pmc $CTRS --kernel-include-regex "${PMC_KERNELS:-k_pool|k_fit|k_chain}" -d gpurun_out/pmc_$SET -o pmc \
+   --output-format csv -- python3 tools/sweep.py --events $EV --pool ${POOL:-32768} --batch ${BATCH:-8} --fit ${FIT:-65536} --reps 1 \
    > gpurun_out/pmc_$SET.log 2>&1
 rc=$?; echo "pmc $SET rc=$rc"; exit $rc

@@ -2,13 +2,15 @@
 """Summarise a rocprofv3 --pmc counter_collection.csv per kernel (totals and per wave)."""
 import collections
 import csv
+import re
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 for r in rows:
-    k = r["Kernel_Name"].split("(")[0][-40:]
+    m = re.search(r"(k_\w+(<\d+>)?)", r["Kernel_Name"])
+    k = m.group(1) if m else r["Kernel_Name"][:40]
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     disp[k].add(r["Dispatch_Id"])
 for k, v in agg.items():

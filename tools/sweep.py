@@ -19,6 +19,7 @@ ap.add_argument("--events", type=int, default=50_000_000)
 ap.add_argument("--fs", type=int, default=5)
 ap.add_argument("--pool", default="8192,16384,32768,65536,131072")
 ap.add_argument("--fit", default="1048576")
+ap.add_argument("--batch", default="8")
 ap.add_argument("--reps", type=int, default=2)
 a = ap.parse_args()
 
@@ -30,9 +31,10 @@ dx, dy = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
 dt, dp = torch.from_numpy(t.view(np.int32)).to(dev), torch.from_numpy(p).to(dev)
 n = len(ev)
 out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev) for c in farms.COLUMNS[4:]}
-for fc in [int(v) for v in a.fit.split(",")]:
-    for pc in [int(v) for v in a.pool.split(",")]:
-        fm = farms.FlowManager(H, W, a.fs, 5, fit_chunk=fc, pool_chunk=pc)
+import itertools  # noqa: E402
+for fc, pc, pb in itertools.product(*[[int(v) for v in s.split(",")] for s in (a.fit, a.pool, a.batch)]):
+    if True:
+        fm = farms.FlowManager(H, W, a.fs, 5, fit_chunk=fc, pool_chunk=pc, pool_batch=pb)
         fm.process_device(dx, dy, dt, dp, out)  # warmup
         best = 1e9
         for _ in range(a.reps):
@@ -46,7 +48,7 @@ for fc in [int(v) for v in a.fit.split(",")]:
         fm.process_device(dx, dy, dt, dp, out)
         st = fm.stats()
         fm.close()
-        print(json.dumps({"fit_chunk": fc, "pool_chunk": pc, "ms": round(best * 1e3, 1),
+        print(json.dumps({"fit_chunk": fc, "pool_chunk": pc, "pool_batch": pb, "ms": round(best * 1e3, 1),
                           "Mev_s": round(n / best / 1e6, 1), "ms_fit_k": round(st["ms_fit_kernel"], 1),
                           "ms_pool_k": round(st["ms_pool_kernel"], 1), "ms_fit_sweep": round(st["ms_fit"], 1),
                           "ms_pool_sweep": round(st["ms_pool"], 1), "ms_prep": round(st["ms_prep"], 1),

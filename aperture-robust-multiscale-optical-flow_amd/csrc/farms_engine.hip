@@ -78,8 +78,8 @@ struct __attribute__((aligned(32))) FlowCell {
 // three or more times in the chunk (a bar's ON/OFF pair is the common case).
 // tag: bit31 = snapshot visited, bits 0..30 = seq of the chunk that last touched
 // the pixel.  e1m: first in-chunk event id, bit31 = more than one in-chunk event.
-// e2m: second in-chunk event id, bit31 = more than two (then tpos[] bounds the
-// pixel's run in P and the out-of-line search resolves it).
+// e2m: second in-chunk event id, bit31 = more than two (then the pixel's run
+// [run_lo, run_hi] of positions in P, scanned in PT, resolves later events).
 struct __attribute__((aligned(16))) SaeCell {
     uint32_t tag;
     uint32_t e1m;
@@ -87,7 +87,7 @@ struct __attribute__((aligned(16))) SaeCell {
     uint32_t tsnap;
     uint32_t e2m;
     uint32_t t2;
-    uint32_t pad0, pad1;
+    int32_t run_lo, run_hi;
 };
 
 // Pooling candidate: one cell of the per-chunk bitmap, its flow state before
@@ -136,7 +136,7 @@ struct Ctx {
     const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
     const int32_t *prev, *next;
     SaeCell *cells;        // SAE snapshot + in-chunk first event, per cell
-    int2 *tpos;            // positions in P of the first / last in-chunk event
+    const int2 *PT;        // per position in P: {event id, t}
     FlowCell *fsnap;       // flow snapshot
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
@@ -162,51 +162,31 @@ struct Ctx {
 };
 
 // ---------------------------------------------------------------------------
-// as-of lookups.  Position in P of the last event at pixel q with id <= e,
-// searched over the pixel's in-chunk run [tpos.x, tpos.y] (rare path: the
-// pixel fired more than once in the chunk and e is past its first event).
-__device__ __forceinline__ int run_search(const Ctx &c, uint32_t q, int e) {
-    const int2 tp = c.tpos[q];
-    int lo = tp.x, hi = tp.y;  // P[lo] <= e
-    if (c.P[hi] <= e) return hi;
-    while (hi - lo > 1) {  // P[lo] <= e < P[hi], P ascending over the run
-        const int mid = (lo + hi) >> 1;
-        if (c.P[mid] <= e) lo = mid;
-        else hi = mid;
+// as-of lookups.  Stamp of the last event with id <= e at a pixel that fired
+// 3+ times in the chunk, given its second in-chunk event (run position
+// lo + 1, stamp t2) is <= e: a short scan of the run's {id, t} pairs.
+__device__ __forceinline__ uint32_t run_asof(const Ctx &c, int lo, int hi, int e, uint32_t t2) {
+    uint32_t t = t2;
+    for (int j = lo + 2; j <= hi; ++j) {
+        const int2 pt = c.PT[j];
+        if (pt.x > e) break;
+        t = (uint32_t)pt.y;
     }
-    return lo;
+    return t;
 }
 
-// SAE stamp of pixel q as of event e (chunk seq) from its loaded cell:
-// -1 never visited, else t; -2 when the pixel fired 3+ times in the chunk and e
-// is past its second event (FAST) — the caller then takes the generic path.
-template <bool FAST>
-__device__ __forceinline__ int64_t sae_resolve(const Ctx &c, const SaeCell &s, uint32_t q, int e, uint32_t seq) {
-    if ((s.tag & kSeqMask) == seq) {
-        const int e1 = (int)(s.e1m & kSeqMask);
-        if (e1 <= e) {
-            if (!(s.e1m >> 31)) return (int64_t)s.t1;
-            const int e2 = (int)(s.e2m & kSeqMask);
-            if (e2 > e) return (int64_t)s.t1;
-            if (!(s.e2m >> 31)) return (int64_t)s.t2;
-            if (FAST) return -2;
-            return (int64_t)c.t[c.P[run_search(c, q, e)]];
-        }
-    }
-    return (s.tag >> 31) ? (int64_t)s.tsnap : int64_t(-1);
-}
-
-// Fast-path form: h is the cell's first 16 B (tag, e1m, t1, tsnap); the
-// second inline event is loaded only when it decides the answer.
+// SAE stamp of pixel q as of event e (chunk seq): -1 never visited, else t.
+// h is the cell's first 16 B (tag, e1m, t1, tsnap); the second half (second
+// event, run bounds) is loaded only when it decides the answer.
 __device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint4 h, uint32_t q, int e, uint32_t seq) {
     if ((h.x & kSeqMask) == seq) {
         const int e1 = (int)(h.y & kSeqMask);
         if (e1 <= e) {
             if (!(h.y >> 31)) return (int64_t)h.z;
-            const uint2 g = reinterpret_cast<const uint2 *>(c.cells)[4 * (size_t)q + 2];  // e2m, t2
+            const uint4 g = reinterpret_cast<const uint4 *>(c.cells)[2 * (size_t)q + 1];  // e2m, t2, run_lo, run_hi
             if ((int)(g.x & kSeqMask) > e) return (int64_t)h.z;
             if (!(g.x >> 31)) return (int64_t)g.y;
-            return -2;
+            return (int64_t)run_asof(c, (int)g.z, (int)g.w, e, g.y);
         }
     }
     return (h.x >> 31) ? (int64_t)h.w : int64_t(-1);
@@ -217,7 +197,7 @@ __device__ __forceinline__ uint4 sae_head(const Ctx &c, uint32_t q) {
 }
 
 __device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
-    return sae_resolve<false>(c, c.cells[q], q, e, seq);
+    return sae_resolve_h(c, sae_head(c, q), q, e, seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -242,12 +222,13 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
     iota[e] = e;
 }
 
-__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next) {
+__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *PT) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n) return;
     const int e = c.P[k];
     const uint32_t q = c.skey[k];
     pos[e] = k;
+    PT[k] = make_int2(e, (int)c.t[e]);
     prev[e] = (k > 0 && c.skey[k - 1] == q) ? c.P[k - 1] : -1;
     next[e] = (k + 1 < c.n && c.skey[k + 1] == q) ? c.P[k + 1] : INT_MAX;
 }
@@ -312,14 +293,14 @@ __global__ void k_fit_prep(Ctx c, int p0, int c0, int c1, uint32_t seq) {
         }
         cell->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
         cell->t1 = c.t[e];
-        c.tpos[q].x = c.pos[e];
+        cell->run_lo = c.pos[e];
         if (nx < c1) {  // and the second one
             const int nn = c.next[nx];
             cell->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
             cell->t2 = c.t[nx];
         }
     }
-    if (nx >= c1) c.tpos[q].y = c.pos[e];
+    if (nx >= c1) c.cells[q].run_hi = c.pos[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -517,7 +498,6 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
     // column's stamps give three vertical partial sums, which are added to the
     // windows whose column range contains it.  Every window's score is the
     // same integer sum in any order.
-    uint32_t slowcol = 0;  // union columns with a cell that needs a run search
     auto load_col = [&](int u0, int v0, int len, uint4 *col) {
         const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
         const int cbase = (u0 - c.X0) * H + v0;
@@ -537,7 +517,6 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
             dd[i] = 0;
             if (v < 0 || v >= H) continue;
             const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
-            if (st == -2) { slowcol |= 1u << (du + 2 * FR); continue; }
             const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
             dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
         }
@@ -559,31 +538,6 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
         load_col(ex + du, ey - 2 * FR, US, ca);
         score_col(du, ca);
     }
-    // rare: the cells of those columns past their pixel's second in-chunk
-    // event, resolved by a run search (the column is re-read to find them)
-    while (slowcol) {
-        const int du = __builtin_ctz(slowcol) - 2 * FR;
-        slowcol &= slowcol - 1;
-        const int u = ex + du;
-        uint4 col[US];
-        load_col(u, ey - 2 * FR, US, col);
-#pragma unroll
-        for (int i = 0; i < US; ++i) {
-            const int dv = i - 2 * FR, v = ey + dv;
-            if (v < 0 || v >= H) continue;
-            const uint32_t q = (uint32_t)((u - c.X0) * H + v);
-            if (sae_resolve_h(c, col[i], q, e, seq) != -2) continue;
-            const int64_t st = sae_asof(c, q, e, seq);
-            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
-#pragma unroll
-            for (int w = 0; w < 9; ++w) {
-                const int ou = (w / 3 - 1) * FR, ov = (w % 3 - 1) * FR;
-                const bool in = du - ou <= FR && ou - du <= FR && dv - ov <= FR && ov - dv <= FR;
-                score[w] += d & -(int64_t)in;  // branch-free: keeps score[] in registers
-            }
-        }
-    }
     const int64_t nn = np;
     int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
     int bw = -1;
@@ -594,17 +548,15 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
 
     // ---- gather the winning window, cx-major (vFlow.cpp:923-930), into LDS
     const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
-    uint64_t vis = 0, wslow = 0;
+    uint64_t vis = 0;
     auto gather_col = [&](int cxo, const uint4 *col) {
         const int u = bi + cxo - FR;
 #pragma unroll
         for (int cyo = 0; cyo < side; ++cyo) {
             const int k = cxo * side + cyo;
             const int64_t st = sae_resolve_h(c, col[cyo], (uint32_t)((u - c.X0) * H + bj - FR + cyo), e, seq);
-            const uint64_t bit = 1ull << k;
-            wslow |= st == -2 ? bit : 0ull;  // selects, not branches: vis / wslow stay in registers
-            vis |= st >= 0 ? bit : 0ull;
-            if (st != -2) lt[k * 256] = st < 0 ? 0u : (uint32_t)st;
+            vis |= st >= 0 ? 1ull << k : 0ull;
+            lt[k * 256] = st < 0 ? 0u : (uint32_t)st;
         }
     };
 #pragma unroll 1
@@ -612,14 +564,6 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
         uint4 ga[side];
         load_col(bi - FR + cxo, bj - FR, side, ga);
         gather_col(cxo, ga);
-    }
-    while (wslow) {
-        const int k = __builtin_ctzll(wslow);
-        wslow &= wslow - 1;
-        const int u = bi + k / side - FR, v = bj + k % side - FR;
-        const int64_t st = sae_asof(c, (uint32_t)((u - c.X0) * H + v), e, seq);
-        lt[k * 256] = st < 0 ? 0u : (uint32_t)st;
-        if (st >= 0) vis |= 1ull << k;
     }
     auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
         const int cx = bi + k / side - FR, cy = bj + k % side - FR;
@@ -1443,7 +1387,7 @@ struct farms_handle {
     hipStream_t stream = nullptr;
     // persistent surfaces (x-major, W*H cells)
     SaeCell *cells = nullptr;
-    int2 *tpos = nullptr;
+    int2 *PT = nullptr;
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
     PoolTouch *ptouch = nullptr;
@@ -1499,7 +1443,7 @@ void dfree(T *&p) {
 
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
-    dfree(h->iota); dfree(h->P); dfree(h->pos); dfree(h->prev); dfree(h->next);
+    dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->pos); dfree(h->prev); dfree(h->next);
     dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
@@ -1522,7 +1466,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
     int rc;
     if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
         (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
-        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->pos, cap)) ||
+        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->pos, cap)) ||
         (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
@@ -1548,7 +1492,6 @@ int ensure_capacity(farms_handle *h, int64_t n) {
 int reset_surfaces(farms_handle *h) {
     // tag 0: never visited, never touched (chunk seqs start at 1)
     HIPCHK(hipMemsetAsync(h->cells, 0, sizeof(SaeCell) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->tpos, 0, sizeof(int2) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ptouch, 0, sizeof(PoolTouch) * 3 * h->WH, h->stream));
@@ -1617,7 +1560,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.pos = h->pos; c.prev = h->prev; c.next = h->next;
     c.Q = h->Q;
-    c.cells = h->cells; c.tpos = h->tpos; c.fsnap = h->fsnap; c.ftime = h->ftime;
+    c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.ptouch = h->ptouch; c.ptpos = h->ptpos;
     c.bm_ring = h->bm_ring; c.blk_ring = h->blk_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk;
@@ -1661,7 +1604,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     size_t bytes = h->cub_bytes;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
                                               end_bit_for(h->WH), s));
-    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next);
+    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next, h->PT);
     {
         int cb = 1;
         while ((1 << cb) < n_pool_chunks) ++cb;
@@ -1873,7 +1816,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
-    if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->tpos, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
+    if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ptouch, 3 * h->WH)) || (rc = dalloc(&h->ptpos, 3 * h->WH)) ||
         (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || (rc = dalloc(&h->blk_ring, (int64_t)h->nblk * h->NB)) ||
         (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->WH * h->NB)) ||
@@ -1890,7 +1833,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     free_workspace(h);
-    dfree(h->cells); dfree(h->tpos); dfree(h->ftime); dfree(h->fsnap);
+    dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
     dfree(h->ptouch); dfree(h->ptpos); dfree(h->bm_ring); dfree(h->blk_ring); dfree(h->wo_ring);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &ev : h->ev)

@@ -68,6 +68,22 @@ def cpu_baseline(ev, width, height, fs, jump, maxw, n_sample):
             "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, {dt:.1f} s"}
 
 
+def pmc_traffic(cfg, world, pool_launches):
+    """HBM bytes per k_pool launch from the committed rocprofv3 PMC passes of the
+    same workload (tools/gpu_traffic.sh -> profiles/rNN_traffic_c<cfg>.json,
+    FETCH_SIZE doubled per the gfx950 correction).  None unless the profile saw
+    exactly this launch count (i.e. the same stream and chunking)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_c{cfg}.json")))
+    if world != 1 or not files:
+        return None
+    k = json.load(open(files[-1]))["kernels"].get("k_pool<11>" if cfg != 5 else "k_pool<3>")
+    if not k or k["dispatches"] != pool_launches:
+        return None
+    return round(k["traffic_bytes_per_launch"])
+
+
 def main():
     args = parse()
     import torch
@@ -151,7 +167,9 @@ def main():
     alg_bytes = 20.0 * st["pool_cells"]  # 20 B per pooled cell of a valid event
     achieved = alg_bytes / (pool_ms / 1e3) / 1e9 if pool_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(cfg, world, pool_launches),
+                "traffic_unit": "HBM bytes per launch (PMC)",
+                "algorithmic_bytes_per_launch": round(alg_bytes / max(pool_launches, 1)),
                 "kernel": "k_pool", "launches_per_step": pool_launches,
                 "avg_launch_us": round(pool_ms * 1e3 / max(pool_launches, 1), 2)}
     line = {

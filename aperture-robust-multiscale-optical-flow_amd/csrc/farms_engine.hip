@@ -108,16 +108,11 @@ struct CandVal {
     int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
 };
 
-// Pooling-sweep touch record of a cell (kept apart from the SAE cells so the
-// pooling chain can run concurrently with the fit sweep): seq of the chunk that
-// last touched the cell, its first in-chunk event | bit31 = more than one.
-struct PoolTouch {
-    uint32_t seq;
-    uint32_t e1m;
-};
-
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
+constexpr int kPoolMaxM = 63;  // largest maxWindow: window rows 2M+1 <= kPoolRowCap
+constexpr int kPoolRowCap = 256;  // row segments (<= 2 per row)
+constexpr int kPoolBitWords = ((2 * kPoolMaxM + 1) * (2 * kPoolMaxM + 1) + 63) / 64;  // flattened positions
 
 struct Ctx {
     int W, H, n;
@@ -141,14 +136,13 @@ struct Ctx {
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
     uint8_t *valid;
-    PoolTouch *ptouch;     // pooling sweep: per-cell touch record, 3 x WH (by chunk % 3)
-    int2 *ptpos;           // pooling sweep: in-chunk run bounds in P, 3 x WH
+    int32_t *pcur, *pend;  // pooling sweep, per cell: cursor into the cell's run of P, last run position (-1: none)
     // ring of NB per-chunk candidate buffers (chunk ch uses buffer ch % NB):
     uint64_t *bm_ring;     // candidate bitmap (nwords per buffer)
-    uint32_t *blk_ring;    // candidates per 1024-cell block (nblk per buffer)
-    uint32_t *wo_ring;     // candidates before each bitmap word (nwords + 1 per buffer)
-    int nblk;
-    CandHdr *hdr_ring;     // compacted candidates, ascending cell index (WH per buffer)
+    uint32_t *wo_ring;     // candidate index of each bitmap word's first candidate (nwords + 1 per buffer)
+    int nblk;              // candidate groups (kGroupCells cells each)
+    int64_t cstride;       // candidate slots per buffer: nblk * kGroupCells
+    CandHdr *hdr_ring;     // candidates of group g at [g * kGroupCells, ...), ascending cell index
     CandVal *val_ring;
     int64_t nwords;
     int NB, C2;            // ring size, events per pooling chunk
@@ -229,8 +223,11 @@ __global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *
     const uint32_t q = c.skey[k];
     pos[e] = k;
     PT[k] = make_int2(e, (int)c.t[e]);
-    prev[e] = (k > 0 && c.skey[k - 1] == q) ? c.P[k - 1] : -1;
-    next[e] = (k + 1 < c.n && c.skey[k + 1] == q) ? c.P[k + 1] : INT_MAX;
+    const bool first = !(k > 0 && c.skey[k - 1] == q), last = !(k + 1 < c.n && c.skey[k + 1] == q);
+    prev[e] = first ? -1 : c.P[k - 1];
+    next[e] = last ? INT_MAX : c.P[k + 1];
+    if (first) c.pcur[q] = k;  // the pooling chain's run bounds of the cell
+    if (last) c.pend[q] = k;
 }
 
 // per pooling chunk: min / max of t (general streams need not be time-sorted)
@@ -872,160 +869,146 @@ __device__ __forceinline__ double xch(double v) {
     return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
 }
 
-constexpr int kBlkCells = 1024;  // cells per candidate-count block (256 threads x 4)
+constexpr int kGroupCells = 1024;  // cells per candidate group (16 bitmap words)
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-    v += (uint32_t)xch32<0>((int)v);
-    v += (uint32_t)xch32<1>((int)v);
-    v += (uint32_t)xch32<2>((int)v);
-    v += (uint32_t)xch32<3>((int)v);
-    v += (uint32_t)xch32<4>((int)v);
-    v += (uint32_t)xch32<5>((int)v);
-    return v;
-}
 
-// Candidate index (in buffer b) of the first candidate with cell index >= L.
-__device__ __forceinline__ uint32_t cand_index(const Ctx &c, int b, int64_t L) {
+// Candidate index (in buffer b) of the first candidate with cell index >= L
+// (cand_lo), and one past the last with cell index <= L (cand_hi); both stay
+// inside L's candidate group.
+__device__ __forceinline__ uint32_t cand_lo(const Ctx &c, int b, int64_t L) {
     const int64_t w = L >> 6;
-    const int r = (int)(L & 63);
-    uint32_t k = c.wo_ring[(int64_t)b * (c.nwords + 1) + w];
-    if (r) k += (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((1ull << r) - 1));
-    return k;
+    return c.wo_ring[(int64_t)b * (c.nwords + 1) + w] +
+           (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((1ull << (L & 63)) - 1));
+}
+__device__ __forceinline__ uint32_t cand_hi(const Ctx &c, int b, int64_t L) {
+    const int64_t w = L >> 6;
+    return c.wo_ring[(int64_t)b * (c.nwords + 1) + w] +
+           (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((2ull << (L & 63)) - 1));
 }
 
-// Candidate record k of buffer b <- cell q: snapshot flow and, if the cell is
-// touched in the chunk (pt.seq == seq), its first in-chunk flow and run bounds.
-__device__ __forceinline__ void fill_cell(const Ctx &c, uint32_t seq, int b, int64_t q, uint32_t k,
-                                          const PoolTouch &pt, int2 run) {
-    const FlowCell snap = c.fsnap[q];
-    CandHdr hd;
-    CandVal v;
-    hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
-    hd.t_snap = snap.t;
-    v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
-    if (pt.seq == seq) {
-        const int e1 = (int)(pt.e1m & kSeqMask);
-        const FlowCell f1 = c.evf[e1];
-        hd.e1 = e1;
-        hd.lin |= (pt.e1m & 0x80000000u ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
-        hd.t1 = f1.t;
-        v.L1 = f1.L; v.Lc1 = f1.Lc; v.Ls1 = f1.Ls;
-        v.run_lo = run.x; v.run_hi = run.y;
-    } else {
-        hd.e1 = INT_MAX;
-        hd.t1 = 0;
-        v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
-        v.run_lo = 0; v.run_hi = 0;
+// The pooling sweep's candidate chain, one launch per super-chunk (pooling
+// chunks [ch0, ch1)).  A block owns one candidate group (kGroupCells = 1024
+// cells = 16 bitmap words; the group's candidates of a chunk take slots
+// [g * 1024, ...) of the chunk's ring buffer, so word offsets need no global
+// scan); wave wv owns words wv, wv + 4, wv + 8, wv + 12, lane = cell.  Each
+// cell's state stays in registers across the chunks: the cursor into its run
+// of P (next event id nxt) and its flow-snapshot stamp ft (-1: snapshot flow
+// invalid).  Per chunk ch (ring buffer ch % NB):
+//   bit(q) = q touched in ch, or ft within the kill time of the chunk's stamp
+//            span: a superset of every cell that can contribute to an event
+//            of ch as of that event (vFlow.cpp:1002/1115);
+//   bitmap word + group-local candidate offsets (block scan of 16 counts);
+//   fill: candidate record = snapshot flow before ch + first in-chunk flow
+//         and the cell's in-chunk run bounds in P;
+//   advance: snapshot <- last in-chunk event at q, cursor past the chunk.
+// Only cells touched in a chunk or carrying a candidate do memory work; the
+// state round-trips memory once per launch.
+__global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
+    __shared__ uint32_t s_cnt[2][16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t g = blockIdx.x;
+    const int n = c.n, C2 = c.C2;
+    const uint64_t lt = (1ull << lane) - 1;
+    int k[4], kend[4], nxt[4];
+    int64_t ft[4];
+    bool dirty[4], bit[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t q = (g * 16 + wv + 4 * i) * 64 + lane;
+        k[i] = 0; kend[i] = -1; ft[i] = -1;
+        if (q < c.WH) { k[i] = c.pcur[q]; kend[i] = c.pend[q]; ft[i] = c.ftime[q]; }
+        nxt[i] = k[i] <= kend[i] ? c.P[k[i]] : INT_MAX;
+        dirty[i] = false;
     }
-    const int64_t kb = (int64_t)b * c.WH + k;
-    c.hdr_ring[kb] = hd;
-    c.val_ring[kb] = v;
-}
-
-// The pooling sweep's candidate chain, one launch per pooling chunk ch:
-//   cell blocks (one cell per thread; candidate counts are kept per group of
-//   kBlkCells = 4 blocks):
-//     - fill: materialise chunk ch's candidate records into ring buffer
-//       ch % NB (its bitmap and per-group counts come from launch ch-1; each
-//       block sums the counts of the groups before it, so there is no scan
-//       pass) and record the candidate offset of each bitmap word;
-//     - flow snapshot <- the last chunk-ch event at each cell ch touched;
-//     - bitmap of chunk ch+1 into buffer (ch+1) % NB: bit q set if q is
-//       touched in ch+1 or its (new) snapshot flow is valid and within the kill
-//       time of some event of ch+1 — a superset of every cell that can
-//       contribute to an event of ch+1 — and the group's candidate count
-//       (atomic adds of the 4 block counts; the group counts of buffer
-//       (ch+2) % NB are cleared here for launch ch+1);
-//   event blocks: first in-chunk event and run bounds of every cell touched by
-//   chunk ch+2 (touch state is triple-buffered by chunk).
-// Launches ch = -2 and -1 prime the chain (touch of chunks 0 and 1, bitmap of 0).
-__global__ __launch_bounds__(256) void k_chain(Ctx c, int ch, int nch, uint32_t seq0) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int ncb = c.nblk * (kBlkCells / 256);  // cell blocks
-    if ((int)blockIdx.x >= ncb) {  // ---- event role: touch chunk ch+2
-        const int tc = ch + 2;
-        if (tc < 0 || tc >= nch) return;
-        const int n0 = tc * c.C2, n1 = min(n0 + c.C2, c.n);
-        const int e = n0 + ((int)blockIdx.x - ncb) * 256 + tid;
-        if (e >= n1) return;
-        const int64_t so = (int64_t)(tc % 3) * c.WH;
-        const uint32_t q = c.pix[e];
-        const int nx = c.next[e];
-        if (c.prev[e] < n0) {
-            c.ptouch[so + q] = PoolTouch{seq0 + (uint32_t)tc, (uint32_t)e | (nx < n1 ? 0x80000000u : 0u)};
-            c.ptpos[so + q].x = c.pos[e];
-        }
-        if (nx >= n1) c.ptpos[so + q].y = c.pos[e];
-        return;
-    }
-    // ---- cell role
-    __shared__ uint32_t s_red[4], s_bef[4], s_off[5];
-    const bool fill = ch >= 0 && ch < nch;
-    const bool next = ch + 1 >= 0 && ch + 1 < nch;
-    const int grp = (int)blockIdx.x >> 2, sub = (int)blockIdx.x & 3;  // group of 1024 cells, block within it
-    const int64_t q = (int64_t)blockIdx.x * 256 + tid;
-    const int64_t w = q >> 6;  // this wave's bitmap word
-    const int b = fill ? ch % c.NB : 0, bn = next ? (ch + 1) % c.NB : 0;
-    const uint32_t seq = seq0 + (uint32_t)ch, seqn = seq + 1u;
-    if (tid == 0 && sub == 0) c.blk_ring[(int64_t)((ch + 2 + c.NB) % c.NB) * c.nblk + grp] = 0;
-    uint64_t bits = 0;
-    uint32_t woff = 0;
-    if (fill) {
-        const uint32_t *blk = c.blk_ring + (int64_t)b * c.nblk;
-        uint32_t before = 0;
-        for (int i = tid; i < grp; i += 256) before += blk[i];
-        before = wave_sum_u32(before);
-        // words of the group before this block's, then this block's 4 words
-        const int64_t gw0 = (int64_t)grp * (kBlkCells / 64);
-        uint32_t pre = 0;
-        if (lane < 4 * sub) pre = gw0 + lane < c.nwords ? (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + gw0 + lane]) : 0u;
-        pre = wave_sum_u32(pre);
-        bits = w < c.nwords ? c.bm_ring[(int64_t)b * c.nwords + w] : 0ull;
-        if (lane == 0) { s_red[wv] = (uint32_t)__popcll(bits); s_bef[wv] = before; }
-        __syncthreads();
-        if (tid == 0) {
-            // groups before: the 4 waves' partial sums; words before in the group:
-            // every wave computed the same `pre`
-            uint32_t run = s_bef[0] + s_bef[1] + s_bef[2] + s_bef[3] + pre;
-            for (int i = 0; i < 4; ++i) { s_off[i] = run; run += s_red[i]; }
-            s_off[4] = run;
-        }
-        __syncthreads();
-        woff = s_off[wv];
-        uint32_t *wo = c.wo_ring + (int64_t)b * (c.nwords + 1);
-        if (lane == 0 && w < c.nwords) wo[w] = woff;
-        if (tid == 0 && (int64_t)blockIdx.x == (c.WH + 255) / 256 - 1) wo[c.nwords] = s_off[4];
-    }
-    bool act = false;
-    if (q < c.WH) {
-        int64_t ft = c.ftime[q];
-        if (fill) {
-            const int64_t so = (int64_t)(ch % 3) * c.WH;
-            const PoolTouch pt = c.ptouch[so + q];
-            const bool touched = pt.seq == seq;
-            int2 run = make_int2(0, 0);
-            if (touched) run = c.ptpos[so + q];
-            if ((bits >> lane) & 1)
-                fill_cell(c, seq, b, q, woff + (uint32_t)__popcll(bits & ((1ull << lane) - 1)), pt, run);
-            if (touched) {  // snapshot <- last event of the chunk at q (after fill read the old one)
-                const FlowCell f = c.evf[c.P[run.y]];
-                c.fsnap[q] = f;
-                ft = f.L > 0 ? (int64_t)f.t : -1;
-                c.ftime[q] = ft;
+    auto mark = [&](int ch) {  // bits of chunk ch from the current state
+        const int ce = min((ch + 1) * C2, n);
+        const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bit[i] = nxt[i] < ce || (ft[i] >= 0 && ft[i] > lo && ft[i] < hi);
+    };
+    mark(ch0);
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const int b = ch % c.NB, par = (ch - ch0) & 1;
+        const int ce = min((ch + 1) * C2, n);
+        uint64_t bal[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bal[i] = __ballot(bit[i]);
+            const int64_t w = g * 16 + wv + 4 * i;
+            if (lane == 0) {
+                s_cnt[par][wv + 4 * i] = (uint32_t)__popcll(bal[i]);
+                if (w < c.nwords) c.bm_ring[(int64_t)b * c.nwords + w] = bal[i];
             }
         }
-        if (next) {
-            const int64_t lo = (int64_t)c.ctmin[ch + 1] - (int64_t)kKillUs;
-            const int64_t hi = (int64_t)c.ctmax[ch + 1] + (int64_t)kKillUs;
-            act = c.ptouch[(int64_t)((ch + 1) % 3) * c.WH + q].seq == seqn || (ft >= 0 && ft > lo && ft < hi);
+        __syncthreads();
+        // exclusive prefix of the group's 16 word counts
+        const uint32_t cw = lane < 16 ? s_cnt[par][lane] : 0u;
+        uint32_t incl = cw;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
+            if (lane >= off) incl += v;
         }
+        const uint32_t excl = incl - cw;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t w = g * 16 + wv + 4 * i;
+            const int64_t q = w * 64 + lane;
+            const uint32_t woff = (uint32_t)(g * kGroupCells) + (uint32_t)__builtin_amdgcn_readlane((int)excl, wv + 4 * i);
+            if (lane == 0 && w < c.nwords) c.wo_ring[(int64_t)b * (c.nwords + 1) + w] = woff;
+            const bool touched = nxt[i] < ce;
+            int e1 = INT_MAX, last = -1;
+            const int k1 = k[i];
+            if (touched) {  // walk the cell's in-chunk run
+                e1 = nxt[i];
+                last = e1;
+                int kk = k1 + 1;
+                int nx = kk <= kend[i] ? c.P[kk] : INT_MAX;
+                while (nx < ce) {
+                    last = nx;
+                    ++kk;
+                    nx = kk <= kend[i] ? c.P[kk] : INT_MAX;
+                }
+                k[i] = kk;
+                nxt[i] = nx;
+            }
+            if (bit[i]) {  // candidate record (snapshot read before the advance below)
+                const FlowCell snap = c.fsnap[q];
+                CandHdr hd;
+                CandVal v;
+                hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
+                hd.t_snap = snap.t;
+                v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
+                if (touched) {
+                    const FlowCell f1 = c.evf[e1];
+                    hd.e1 = e1;
+                    hd.lin |= (k[i] - 1 > k1 ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
+                    hd.t1 = f1.t;
+                    v.L1 = f1.L; v.Lc1 = f1.Lc; v.Ls1 = f1.Ls;
+                    v.run_lo = k1; v.run_hi = k[i] - 1;
+                } else {
+                    hd.e1 = INT_MAX;
+                    hd.t1 = 0;
+                    v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
+                    v.run_lo = 0; v.run_hi = 0;
+                }
+                const int64_t kb = (int64_t)b * c.cstride + woff + (uint32_t)__popcll(bal[i] & lt);
+                c.hdr_ring[kb] = hd;
+                c.val_ring[kb] = v;
+            }
+            if (touched) {  // snapshot <- last event of the chunk at q
+                const FlowCell f = c.evf[last];
+                c.fsnap[q] = f;
+                ft[i] = f.L > 0 ? (int64_t)f.t : -1;
+                dirty[i] = true;
+            }
+        }
+        if (ch + 1 < ch1) mark(ch + 1);
     }
-    if (next) {
-        const uint64_t bal = __ballot(act);
-        if (lane == 0) {
-            if (w < c.nwords) c.bm_ring[(int64_t)bn * c.nwords + w] = bal;
-            if (bal) atomicAdd(&c.blk_ring[(int64_t)bn * c.nblk + grp], (uint32_t)__popcll(bal));
-        }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t q = (g * 16 + wv + 4 * i) * 64 + lane;
+        if (dirty[i]) { c.ftime[q] = ft[i]; c.pcur[q] = k[i]; }
     }
 }
 
@@ -1099,17 +1082,20 @@ __device__ __forceinline__ double wave_max(double v) {
 // contributor sets give identical scale sums (tie rule of vFlow.cpp:1161).
 template <int K>
 __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
-    __shared__ int s_pre[4][130];       // per wave: prefix of candidate counts over rows
-    __shared__ int s_skip[4][128];      // per wave: candidate index - flattened index, per row
-    __shared__ uint2 s_con[4][kPoolCap];  // per wave: contributors {ref, kind | k0 << 8}
+    // per wave: bit f set iff a non-empty row segment starts at flattened
+    // candidate position f; the non-empty segments in order {row, candidate
+    // index - flattened index}; the staged contributors {ref, kind | k0 << 8}
+    __shared__ uint64_t s_start[4][kPoolBitWords];
+    __shared__ int2 s_row[4][kPoolRowCap];
+    __shared__ uint2 s_con[4][kPoolCap];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     if (w >= c1) return;
     const int e = c.Q[w];  // events of the chunk in tile order
     if (!c.valid[e]) return;
     const int buf = (w / c.C2) % c.NB;  // this event's chunk's candidate buffer
-    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.WH;
-    const CandVal *cval = c.val_ring + (int64_t)buf * c.WH;
+    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
+    const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
     const int ex = c.x[e], ey = c.y[e];
     if (ex < c.own_lo || ex >= c.own_hi) return;  // halo event: fitted, pooled by its owner
     const uint32_t teu = c.t[e];
@@ -1118,12 +1104,22 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     const int WHs = (int)c.WHs;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    const int nrows = i_hi - i_lo + 1;  // <= 2M+1
-    // ---- per-row candidate slices and their prefix
-    int carry = 0;
+    const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= kPoolRowCap / 2
+    // ---- per-row candidate slices: flattened start of each non-empty row as a
+    // bit of s_start, and its candidate offset in s_row
+    uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start[wv]);
+    {
+        const int nw = (nrows * (j_hi - j_lo + 1) + 63) >> 6;  // bound on the flattened length, in words
+        for (int i = lane; i < nw; i += 64) s_start[wv][i] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // A row's cell range maps to one candidate slice per candidate group it
+    // overlaps (ranges are shorter than a group: at most two segments).
+    int carry = 0, nz = 0;
     for (int r0 = 0; r0 < nrows; r0 += 64) {
         const int r = r0 + lane;
-        int a = 0, cnt = 0;
+        int a0 = 0, n0 = 0, a1 = 0, n1 = 0;
         if (r < nrows) {
             const int base = (i_lo + r) * H;
             int l1 = base + j_hi;
@@ -1133,23 +1129,40 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
             if (l0 < 0) l0 = 0;               // outside the stored region: never visited
             if (l1 > WHl - 1) l1 = WHl - 1;
             if (l0 <= l1) {
-                a = (int)cand_index(c, buf, l0);
-                cnt = (int)cand_index(c, buf, l1 + 1) - a;
+                const int gb = l1 & ~(kGroupCells - 1);  // first cell of l1's group
+                a0 = (int)cand_lo(c, buf, l0);
+                if (l0 < gb) {
+                    n0 = (int)cand_hi(c, buf, gb - 1) - a0;
+                    a1 = (int)cand_lo(c, buf, gb);
+                    n1 = (int)cand_hi(c, buf, l1) - a1;
+                } else {
+                    n0 = (int)cand_hi(c, buf, l1) - a0;
+                }
             }
         }
+        const int cnt = n0 + n1;
         int incl = cnt;  // inclusive wave scan
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const int v = __shfl_up(incl, off, 64);
             if (lane >= off) incl += v;
         }
-        if (r < nrows) {
-            s_pre[wv][r + 1] = carry + incl;
-            s_skip[wv][r] = a - (carry + incl - cnt);
+        const int start = carry + incl - cnt;
+        const uint64_t lt = (1ull << lane) - 1;
+        const uint64_t b0 = __ballot(n0 > 0), b1 = __ballot(n1 > 0);
+        int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
+        if (n0 > 0) {
+            s_row[wv][idx++] = make_int2(r, a0 - start);
+            atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
+        if (n1 > 0) {
+            const int st1 = start + n0;
+            s_row[wv][idx] = make_int2(r, a1 - st1);
+            atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
+        }
+        nz += (int)__popcll(b0) + (int)__popcll(b1);
         carry += __shfl(incl, 63, 64);
     }
-    if (lane == 0) s_pre[wv][0] = 0;
     // the LDS arrays are private to this wave: a wavefront-scope fence orders
     // the writes above before the reads below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1161,26 +1174,17 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     auto collect = [&](int pass) -> int {
         const int rank_lo = pass * kPoolCap, rank_hi = rank_lo + kPoolCap;
         int ncon = 0;
-        // Rows of the flattened window [fw, fw + 64): lane f's row is r0 plus
-        // the number of row ends s_pre[r0 + d + 1] <= f.  Each lane loads one
-        // upcoming row end and the wave walks them by readlane (uniform loop),
-        // which also advances r0 to the row of fw + 64.
-        int r0 = 0;
+        // Flattened positions [fw, fw + 64) (fw a multiple of 64, steps in
+        // order): lane f's segment is the last non-empty one starting at or
+        // before f, i.e. the (number of segment starts <= f)-th one.
+        int mbase = 0;  // non-empty segments starting before fw
         auto locate = [&](int fw, int f, int &row, int &k) {
-            int r = r0;
-            for (int base = r0;;) {
-                const int myb = base + lane < nrows ? s_pre[wv][base + lane + 1] : INT_MAX;
-                int d = 0;
-                for (; d < 64; ++d) {
-                    const int bnd = __builtin_amdgcn_readlane(myb, d);
-                    if (bnd > fw + 64) break;
-                    r += f >= bnd ? 1 : 0;
-                }
-                base += d;
-                if (d < 64) { r0 = base; break; }
-            }
-            row = r;
-            k = f + s_skip[wv][r < nrows ? r : nrows - 1];
+            const uint64_t mk = s_start[wv][fw >> 6];
+            const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
+            mbase += (int)__popcll(mk);
+            const int2 rs = s_row[wv][m < 0 ? 0 : m];
+            row = rs.x;
+            k = f + rs.y;
         };
         // software pipeline: the header of step s+1 is in flight while step s
         // is resolved
@@ -1390,13 +1394,13 @@ struct farms_handle {
     int2 *PT = nullptr;
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    PoolTouch *ptouch = nullptr;
-    int2 *ptpos = nullptr;
+    int32_t *pcur = nullptr, *pend = nullptr;
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1)
     int pool_batch = 16, NB = 33;
     uint64_t *bm_ring = nullptr;
-    uint32_t *blk_ring = nullptr, *wo_ring = nullptr;
+    uint32_t *wo_ring = nullptr;
     int nblk = 0;
+    int64_t cstride = 0;
     CandHdr *hdr_ring = nullptr;
     CandVal *val_ring = nullptr;
     int64_t nwords = 0;
@@ -1494,7 +1498,6 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipMemsetAsync(h->cells, 0, sizeof(SaeCell) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->ptouch, 0, sizeof(PoolTouch) * 3 * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     return FARMS_OK;
@@ -1562,8 +1565,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.Q = h->Q;
     c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
-    c.ptouch = h->ptouch; c.ptpos = h->ptpos;
-    c.bm_ring = h->bm_ring; c.blk_ring = h->blk_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk;
+    c.pcur = h->pcur; c.pend = h->pend;
+    c.bm_ring = h->bm_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
@@ -1604,6 +1607,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     size_t bytes = h->cub_bytes;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
                                               end_bit_for(h->WH), s));
+    HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
     hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next, h->PT);
     {
         int cb = 1;
@@ -1655,14 +1659,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         return FARMS_OK;
     };
-    const uint32_t pseq0 = h->seq + 1;  // pooling chunk ch has sequence pseq0 + ch
-    h->seq += (uint32_t)n_pool_chunks + 2;
-    const int chain_grid = h->nblk * (kBlkCells / 256) + ceil_div(h->pool_chunk, 256);
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
-    if (n_pool_chunks > 0) {  // prime: touch chunks 0 and 1, bitmap of chunk 0
-        hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, -2, n_pool_chunks, pseq0);
-        hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, -1, n_pool_chunks, pseq0);
-    }
     int fit_enqueued = 0, fit_waited = -1;
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
@@ -1674,11 +1671,12 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             if (rc) return rc;
         }
         if (S >= 2) HIPCHK(hipStreamWaitEvent(sc, ev_pool(S - 2), 0));  // ring buffers of S-2 are free
-        for (int ch = ch0; ch < ch1; ++ch) {
-            const int f = (int)((int64_t)ch * h->pool_chunk / h->fit_chunk);  // fit chunks are whole pooling chunks
-            if (f > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(f), 0)); fit_waited = f; }
-            hipLaunchKernelGGL(k_chain, dim3(chain_grid), dim3(256), 0, sc, c, ch, n_pool_chunks, pseq0);
+        {  // the chain reads the local flows of every event of the super-chunk
+            const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
+            const int fl = std::min(f, n_fit_chunks - 1);
+            if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
+        hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(256), 0, sc, c, ch0, ch1);
         HIPCHK(hipEventRecord(ev_cand(S), sc));
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
@@ -1774,6 +1772,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // spatialPool has maxWindow slots and is indexed with .at() (vFlow.cpp:966,1025)
     if (K > prm->max_window) return fail(FARMS_EINVAL, "more pooling scales than maxWindow (reference throws)");
     if (K > kMaxScales) return fail(FARMS_EINVAL, "at most 16 pooling scales are supported");
+    if (prm->max_window > kPoolMaxM) return fail(FARMS_EINVAL, "maxWindow above 63 is not supported");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(FARMS_ENODEV, "no HIP device");
     if (prm->device < 0 || prm->device >= ndev) return fail(FARMS_ENODEV, "device ordinal out of range");
@@ -1797,7 +1796,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (prm->pool_batch > 0) h->pool_batch = prm->pool_batch;
     h->NB = 2 * h->pool_batch + 1;
     h->nwords = (h->WH + 63) / 64;
-    h->nblk = (int)((h->WH + 1023) / 1024);
+    h->nblk = (int)((h->WH + kGroupCells - 1) / kGroupCells);
+    h->cstride = (int64_t)h->nblk * kGroupCells;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     {
@@ -1817,10 +1817,10 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ptouch, 3 * h->WH)) || (rc = dalloc(&h->ptpos, 3 * h->WH)) ||
-        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || (rc = dalloc(&h->blk_ring, (int64_t)h->nblk * h->NB)) ||
-        (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->WH * h->NB)) ||
-        (rc = dalloc(&h->val_ring, h->WH * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->pcur, h->WH)) || (rc = dalloc(&h->pend, h->WH)) ||
+        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || 
+        (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
+        (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
@@ -1834,7 +1834,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     free_workspace(h);
     dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
-    dfree(h->ptouch); dfree(h->ptpos); dfree(h->bm_ring); dfree(h->blk_ring); dfree(h->wo_ring);
+    dfree(h->pcur); dfree(h->pend); dfree(h->bm_ring); dfree(h->wo_ring);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);

@@ -60,7 +60,8 @@ constexpr double kMaxStamp = 4294967296.0;  // vFlow.h:27
 constexpr double kTsToSec = 1e-6;           // vFlow.h:28
 constexpr double kKillUs = 500.0;           // vFlow.cpp:961
 constexpr int kDefaultFitChunk = 1 << 16;
-constexpr int kDefaultPoolChunk = 1 << 14;
+constexpr int kDefaultPoolChunk = 1 << 13;
+constexpr int kDefaultPoolBatch = 64;  // pooling chunks per super-chunk (ring of 2B+1 candidate buffers)
 constexpr int kMaxScales = 16;
 
 // Local-flow state of one event, and the flow surface cell (x-major).  L = 0 for
@@ -940,7 +941,9 @@ __global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
                 if (w < c.nwords) c.bm_ring[(int64_t)b * c.nwords + w] = bal[i];
             }
         }
-        __syncthreads();
+        // block barrier for the word counts in LDS only: the global stores of
+        // this chunk are read by later kernels, not by other waves here
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         // exclusive prefix of the group's 16 word counts
         const uint32_t cw = lane < 16 ? s_cnt[par][lane] : 0u;
         uint32_t incl = cw;
@@ -956,31 +959,38 @@ __global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
             const int64_t q = w * 64 + lane;
             const uint32_t woff = (uint32_t)(g * kGroupCells) + (uint32_t)__builtin_amdgcn_readlane((int)excl, wv + 4 * i);
             if (lane == 0 && w < c.nwords) c.wo_ring[(int64_t)b * (c.nwords + 1) + w] = woff;
+            // the loads of the common case (one event at q in the chunk) are
+            // issued together: the run's next id, the first in-chunk flow, the
+            // old snapshot; a longer run is walked afterwards
             const bool touched = nxt[i] < ce;
-            int e1 = INT_MAX, last = -1;
             const int k1 = k[i];
-            if (touched) {  // walk the cell's in-chunk run
-                e1 = nxt[i];
-                last = e1;
-                int kk = k1 + 1;
-                int nx = kk <= kend[i] ? c.P[kk] : INT_MAX;
-                while (nx < ce) {
-                    last = nx;
-                    ++kk;
-                    nx = kk <= kend[i] ? c.P[kk] : INT_MAX;
-                }
-                k[i] = kk;
-                nxt[i] = nx;
+            const int e1 = touched ? nxt[i] : INT_MAX;
+            int nx = INT_MAX;
+            FlowCell f1{}, snap{};
+            if (touched) {
+                if (k1 + 1 <= kend[i]) nx = c.P[k1 + 1];
+                f1 = c.evf[e1];
             }
-            if (bit[i]) {  // candidate record (snapshot read before the advance below)
-                const FlowCell snap = c.fsnap[q];
+            if (bit[i]) snap = c.fsnap[q];
+            FlowCell fl = f1;  // flow of the last in-chunk event at q
+            if (touched) {
+                int kk = k1 + 1, last = e1, nn = nx;
+                while (nn < ce) {
+                    last = nn;
+                    ++kk;
+                    nn = kk <= kend[i] ? c.P[kk] : INT_MAX;
+                }
+                if (last != e1) fl = c.evf[last];
+                k[i] = kk;
+                nxt[i] = nn;
+            }
+            if (bit[i]) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
                 CandHdr hd;
                 CandVal v;
                 hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
                 hd.t_snap = snap.t;
                 v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
                 if (touched) {
-                    const FlowCell f1 = c.evf[e1];
                     hd.e1 = e1;
                     hd.lin |= (k[i] - 1 > k1 ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
                     hd.t1 = f1.t;
@@ -997,9 +1007,8 @@ __global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
                 c.val_ring[kb] = v;
             }
             if (touched) {  // snapshot <- last event of the chunk at q
-                const FlowCell f = c.evf[last];
-                c.fsnap[q] = f;
-                ft[i] = f.L > 0 ? (int64_t)f.t : -1;
+                c.fsnap[q] = fl;
+                ft[i] = fl.L > 0 ? (int64_t)fl.t : -1;
                 dirty[i] = true;
             }
         }
@@ -1080,25 +1089,16 @@ __device__ __forceinline__ double wave_max(double v) {
 // The summation order depends only on the contributor list, so results are
 // bitwise independent of chunking and streaming splits, and identical
 // contributor sets give identical scale sums (tie rule of vFlow.cpp:1161).
+// Pooling of one valid owned event e at (ex, ey, teu) by the calling wave,
+// against candidate buffer buf.  LDS (private to the wave): s_start bit f set
+// iff a non-empty row segment starts at flattened candidate position f;
+// s_row the non-empty segments in order {row, candidate index - flattened
+// index}; s_con the staged contributors {ref, kind | k0 << 8}.
 template <int K>
-__global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
-    // per wave: bit f set iff a non-empty row segment starts at flattened
-    // candidate position f; the non-empty segments in order {row, candidate
-    // index - flattened index}; the staged contributors {ref, kind | k0 << 8}
-    __shared__ uint64_t s_start[4][kPoolBitWords];
-    __shared__ int2 s_row[4][kPoolRowCap];
-    __shared__ uint2 s_con[4][kPoolCap];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (w >= c1) return;
-    const int e = c.Q[w];  // events of the chunk in tile order
-    if (!c.valid[e]) return;
-    const int buf = (w / c.C2) % c.NB;  // this event's chunk's candidate buffer
+__device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
+                                           uint64_t *s_start, int2 *s_row, uint2 *s_con) {
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
-    const int ex = c.x[e], ey = c.y[e];
-    if (ex < c.own_lo || ex >= c.own_hi) return;  // halo event: fitted, pooled by its owner
-    const uint32_t teu = c.t[e];
     const int W = c.W, H = c.H, M = c.M, J = c.J;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
     const int WHs = (int)c.WHs;
@@ -1107,10 +1107,10 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= kPoolRowCap / 2
     // ---- per-row candidate slices: flattened start of each non-empty row as a
     // bit of s_start, and its candidate offset in s_row
-    uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start[wv]);
+    uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
     {
         const int nw = (nrows * (j_hi - j_lo + 1) + 63) >> 6;  // bound on the flattened length, in words
-        for (int i = lane; i < nw; i += 64) s_start[wv][i] = 0;
+        for (int i = lane; i < nw; i += 64) s_start[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1152,12 +1152,12 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
         const uint64_t b0 = __ballot(n0 > 0), b1 = __ballot(n1 > 0);
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
         if (n0 > 0) {
-            s_row[wv][idx++] = make_int2(r, a0 - start);
+            s_row[idx++] = make_int2(r, a0 - start);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
         if (n1 > 0) {
             const int st1 = start + n0;
-            s_row[wv][idx] = make_int2(r, a1 - st1);
+            s_row[idx] = make_int2(r, a1 - st1);
             atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
         }
         nz += (int)__popcll(b0) + (int)__popcll(b1);
@@ -1179,10 +1179,10 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
         // before f, i.e. the (number of segment starts <= f)-th one.
         int mbase = 0;  // non-empty segments starting before fw
         auto locate = [&](int fw, int f, int &row, int &k) {
-            const uint64_t mk = s_start[wv][fw >> 6];
+            const uint64_t mk = s_start[fw >> 6];
             const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
             mbase += (int)__popcll(mk);
-            const int2 rs = s_row[wv][m < 0 ? 0 : m];
+            const int2 rs = s_row[m < 0 ? 0 : m];
             row = rs.x;
             k = f + rs.y;
         };
@@ -1225,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
             const uint64_t bal = __ballot(con);
             if (con) {
                 const int rank = ncon + (int)__popcll(bal & ((1ull << lane) - 1));
-                if (rank >= rank_lo && rank < rank_hi) s_con[wv][rank - rank_lo] = make_uint2(ref, meta);
+                if (rank >= rank_lo && rank < rank_hi) s_con[rank - rank_lo] = make_uint2(ref, meta);
             }
             ncon += (int)__popcll(bal);
             hc = hn; rc = rn; kc = kn;
@@ -1233,6 +1233,18 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         return ncon;
+    };
+    auto length_of = [&](uint2 en) -> double {
+        const uint32_t kind = en.y & 0xFF;
+        if (kind == 0) return cval[en.x].L_snap;
+        if (kind == 1) return cval[en.x].L1;
+        return c.evf[en.x].L;
+    };
+    auto vec_of = [&](uint2 en, double &Lc, double &Ls) {
+        const uint32_t kind = en.y & 0xFF;
+        if (kind == 0) { Lc = cval[en.x].Lc_snap; Ls = cval[en.x].Ls_snap; }
+        else if (kind == 1) { Lc = cval[en.x].Lc1; Ls = cval[en.x].Ls1; }
+        else { Lc = c.evf[en.x].Lc; Ls = c.evf[en.x].Ls; }
     };
     auto value_of = [&](uint2 en, double &L, double &Lc, double &Ls) {
         const uint32_t kind = en.y & 0xFF;
@@ -1242,8 +1254,11 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     };
     // ---- phase B1: length sum and count per scale; lane l takes a contiguous
     // share of each staged batch
+    constexpr int kShare = kPoolCap / 64;
     double sL[K];
     int cntk[K];
+    double vL[kShare];  // the lane's staged lengths (last pass)
+    int vk0[kShare];
 #pragma unroll
     for (int k = 0; k < K; ++k) { sL[k] = 0.0; cntk[k] = 0; }
     int npass = 1, ncon_total = 0;
@@ -1255,14 +1270,23 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
         ncon_total = collect(pass);
         npass = ncon_total > kPoolCap ? (ncon_total + kPoolCap - 1) / kPoolCap : 1;
         const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
-        for (int b = nb * lane / 64; b < nb * (lane + 1) / 64; ++b) {
-            const uint2 en = s_con[wv][b];
-            const int k0 = (int)(en.y >> 8);
-            double L, Lc, Ls;
-            value_of(en, L, Lc, Ls);
+        // this lane's share (<= kShare entries): all value loads in flight together
+        const int b0 = nb * lane / 64, b1 = nb * (lane + 1) / 64;
+#pragma unroll
+        for (int j = 0; j < kShare; ++j) {
+            vk0[j] = K;  // empty slot: in no scale
+            vL[j] = 0.0;
+            if (b0 + j < b1) {
+                const uint2 en = s_con[b0 + j];
+                vk0[j] = (int)(en.y >> 8);
+                vL[j] = length_of(en);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kShare; ++j) {
 #pragma unroll
             for (int kk = 0; kk < K; ++kk)
-                if (kk >= k0) { sL[kk] += L; cntk[kk] += 1; }
+                if (kk >= vk0[j]) { sL[kk] += vL[j]; cntk[kk] += 1; }
         }
     }
     // wave totals: slot 2k = length sum of scale k, slot 2k+1 = its count
@@ -1290,7 +1314,18 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
     }
     // ---- phase B2: mean vector of the winning scale (vFlow.cpp:1067-1075)
     double sXY[2] = {0.0, 0.0};
-    if (maxv > 0) {
+    if (maxv > 0 && npass == 1) {  // the batch is still staged; the lane's scales are in registers
+        const int b0 = ncon_total * lane / 64;
+        double vC[kShare], vS[kShare];
+#pragma unroll
+        for (int j = 0; j < kShare; ++j) {
+            vC[j] = 0.0; vS[j] = 0.0;
+            if (vk0[j] <= mi) vec_of(s_con[b0 + j], vC[j], vS[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kShare; ++j)
+            if (vk0[j] <= mi) { sXY[0] += vC[j]; sXY[1] += vS[j]; }
+    } else if (maxv > 0) {
         for (int pass = 0; pass < npass; ++pass) {
             if (npass > 1) {  // re-stage batch `pass` (a single batch is still in LDS)
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1299,7 +1334,7 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
             }
             const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
             for (int b = nb * lane / 64; b < nb * (lane + 1) / 64; ++b) {
-                const uint2 en = s_con[wv][b];
+                const uint2 en = s_con[b];
                 if ((int)(en.y >> 8) <= mi) {
                     double L, Lc, Ls;
                     value_of(en, L, Lc, Ls);
@@ -1322,11 +1357,45 @@ __global__ __launch_bounds__(256) void k_pool(Ctx c, int c0, int c1) {
             const FlowCell self = c.evf[e];
             gx = self.Lc; gy = self.Ls; sc = 0;
         }
-        c.r_true[e] = sqrt(gy * gy + gx * gx);  // vFlow.cpp:365-366
-        c.th_true[e] = atan2(gy, gx);
+        c.r_true[e] = gx;  // (RTrue, ThetaTrue) by k_true_polar, 64 events per wave
+        c.th_true[e] = gy;
         c.scale[e] = sc;
         if (c.dbg_tc) c.dbg_tc[e] = make_int2(total, ncon_total);
     }
+}
+
+// One wavefront per work-order position of [c0, c1) (events of a chunk in
+// tile order); invalid events and halo events (fitted here, pooled by their
+// owner) leave at once.
+#ifndef FARMS_POOL_WAVES
+#define FARMS_POOL_WAVES 1  // minimum waves per SIMD requested of the register allocator
+#endif
+template <int K>
+__global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
+    __shared__ uint64_t s_start[4][kPoolBitWords];
+    __shared__ int2 s_row[4][kPoolRowCap];
+    __shared__ uint2 s_con[4][kPoolCap];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (w >= c1) return;
+    const int e = c.Q[w];
+    if (!c.valid[e]) return;
+    const int ex = c.x[e];
+    if (ex < c.own_lo || ex >= c.own_hi) return;
+    const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
+    pool_event<K>(c, e, ex, c.y[e], c.t[e], buf, lane, s_start[wv], s_row[wv], s_con[wv]);
+}
+
+// Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
+// owned) event: k_pool leaves (Gx, Gy) in the r_true / theta_true columns.
+__global__ void k_true_polar(Ctx c) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= c.n || !c.valid[e]) return;
+    const int x = c.x[e];
+    if (x < c.own_lo || x >= c.own_hi) return;
+    const double gx = c.r_true[e], gy = c.th_true[e];
+    c.r_true[e] = sqrt(gy * gy + gx * gx);
+    c.th_true[e] = atan2(gy, gx);
 }
 
 // lastEventTime surface for farms_get_last_event_time: stamp of the latest
@@ -1396,7 +1465,7 @@ struct farms_handle {
     FlowCell *fsnap = nullptr;
     int32_t *pcur = nullptr, *pend = nullptr;
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1)
-    int pool_batch = 16, NB = 33;
+    int pool_batch = kDefaultPoolBatch, NB = 2 * kDefaultPoolBatch + 1;
     uint64_t *bm_ring = nullptr;
     uint32_t *wo_ring = nullptr;
     int nblk = 0;
@@ -1425,7 +1494,8 @@ struct farms_handle {
     size_t cub_bytes = 0;
     int *err = nullptr;
     unsigned long long *counters = nullptr;
-    bool profiling = false;
+    bool profiling = false;  // kernel timing events
+    bool counting = false;   // work counters (k_stats, per-event candidate counts)
     hipEvent_t ev[8] = {};
     std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
     farms_stats stats{};
@@ -1574,7 +1644,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
     if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
     c.counters = h->counters;
-    c.dbg_tc = h->profiling ? h->dbg_tc : nullptr;
+    c.dbg_tc = h->counting ? h->dbg_tc : nullptr;
 
     const bool prof = h->profiling;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
@@ -1697,8 +1767,9 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
     }
+    if (n_super > 0) hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
-    if (prof) {
+    if (h->counting) {
         HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 5, s));
         hipLaunchKernelGGL(k_stats, dim3(1024), dim3(256), 0, s, c);
     }
@@ -1731,6 +1802,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         st.ms_fit_kernel = kf;
         st.ms_pool_kernel = kp;
+    }
+    if (h->counting) {
         unsigned long long cnt[5];
         HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
         st.n_valid = (int64_t)cnt[0];
@@ -1856,6 +1929,7 @@ extern "C" int farms_reset(farms_handle *h) {
 extern "C" int farms_set_profiling(farms_handle *h, int enable) {
     if (!h) return fail(FARMS_EINVAL, "null handle");
     h->profiling = enable != 0;
+    h->counting = enable != 0 && enable != FARMS_PROF_TIMING;
     return FARMS_OK;
 }
 

@@ -24,6 +24,8 @@ FARMS_EINVAL = -1
 FARMS_EHIP = -2
 FARMS_ENOMEM = -3
 FARMS_ENODEV = -4
+PROF_TIMING = 1    # farms_set_profiling: HIP events around phases and k_fit / k_pool launches
+PROF_COUNTERS = 2  # ... plus the U_loc / U_pool / candidate / contributor counters
 
 # record columns, in the order of src/vFlow.cpp:438
 COLUMNS = ("x", "y", "t", "p", "r_true", "theta_true", "vx", "vy", "r_local", "theta_local", "scale")
@@ -122,9 +124,15 @@ def load_hip_library() -> ctypes.CDLL:
     global _hip
     if _hip is not None:
         return _hip
-    if not os.path.exists(HIP_LIB):
-        raise FarmsError(FARMS_ENODEV, f"{HIP_LIB} not built; run __graft_entry__.build()")
-    lib = ctypes.CDLL(HIP_LIB)
+    # FARMS_HIP_LIB: an alternative build of the same library (tuning A/B runs
+    # of tools/, e.g. `make -C ... variant NAME=x DEFS=...`); never set by the
+    # tests, the bench or the driver entry points
+    path = os.environ.get("FARMS_HIP_LIB") or HIP_LIB
+    if not os.path.isabs(path):
+        path = os.path.join(HERE, path)
+    if not os.path.exists(path):
+        raise FarmsError(FARMS_ENODEV, f"{path} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
     lib.farms_last_error.restype = ctypes.c_char_p
     for name in HIP_SYMBOLS:
         if name != "farms_last_error":
@@ -309,8 +317,9 @@ class FlowManager:
     def reset(self) -> None:
         _check(self._lib, self._lib.farms_reset(self._h))
 
-    def set_profiling(self, on: bool) -> None:
-        _check(self._lib, self._lib.farms_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on: bool | int) -> None:
+        """True: timing events and work counters; PROF_TIMING: timing only."""
+        _check(self._lib, self._lib.farms_set_profiling(self._h, int(on) if not isinstance(on, bool) else (3 if on else 0)))
 
     def stats(self) -> dict:
         st = FarmsStats()

@@ -56,7 +56,7 @@ typedef struct {
      * sensor), owned records are bitwise those of a whole-sensor run. */
     int32_t region_x0, region_width;
     int32_t own_x0, own_x1;
-    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (16) */
+    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64) */
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA
@@ -110,8 +110,13 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
                          const uint32_t *d_t_rel, const int32_t *d_p, int64_t n,
                          farms_records *d_out);
 
-/* Record HIP events around every kernel of the next calls (per-kernel times in
- * farms_stats).  0 = off (default). */
+/* Profiling of the next calls: FARMS_PROF_TIMING records HIP events around the
+ * phases and every k_fit / k_pool launch (times in farms_stats; negligible
+ * cost), FARMS_PROF_COUNTERS also counts U_loc / U_pool / candidates /
+ * contributors (an extra kernel pass, ~2% of a call).  0 = off (default); any
+ * other nonzero value = both. */
+#define FARMS_PROF_TIMING 1
+#define FARMS_PROF_COUNTERS 2
 int farms_set_profiling(farms_handle *h, int enable);
 int farms_get_stats(const farms_handle *h, farms_stats *out);
 

@@ -917,7 +917,11 @@ __global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
     for (int i = 0; i < 4; ++i) {
         const int64_t q = (g * 16 + wv + 4 * i) * 64 + lane;
         k[i] = 0; kend[i] = -1; ft[i] = -1;
-        if (q < c.WH) { k[i] = c.pcur[q]; kend[i] = c.pend[q]; ft[i] = c.ftime[q]; }
+        if (q < c.WH) {
+            kend[i] = c.pend[q];
+            if (kend[i] >= 0) k[i] = c.pcur[q];  // pcur is only defined for cells with events in this call
+            ft[i] = c.ftime[q];
+        }
         nxt[i] = k[i] <= kend[i] ? c.P[k[i]] : INT_MAX;
         dirty[i] = false;
     }
@@ -1398,6 +1402,47 @@ __global__ void k_true_polar(Ctx c) {
     c.th_true[e] = atan2(gy, gx);
 }
 
+// ---------------------------------------------------------------------------
+// Temporal segments (multi-GPU): the SAE a segment starts from.
+// Last event index per pixel (x-major, whole sensor), then its stamp.
+__global__ void k_last_index(const int32_t *x, const int32_t *y, int e0, int e1, int W, int H, int32_t *last) {
+    const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= e1) return;
+    const int ex = x[e], ey = y[e];
+    if (ex < 0 || ex >= W || ey < 0 || ey >= H) return;  // rejected by farms_process* anyway
+    atomicMax(&last[(int64_t)ex * H + ey], e);
+}
+
+__global__ void k_last_stamp(const int32_t *last, const uint32_t *t, int64_t WH, int64_t *out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= WH) return;
+    const int e = last[q];
+    out[q] = e >= 0 ? (int64_t)t[e] : int64_t(-1);
+}
+
+// out[q] = the stamp of the last array (in order) that visited q, -1 if none.
+__global__ void k_merge_stamps(const int64_t *in, int count, int64_t WH, int64_t *out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= WH) return;
+    int64_t v = -1;
+    for (int i = 0; i < count; ++i) {
+        const int64_t s = in[(int64_t)i * WH + q];
+        v = s >= 0 ? s : v;
+    }
+    out[q] = v;
+}
+
+// SAE snapshot of the stored region <- whole-sensor stamps (-1: never visited).
+__global__ void k_seed_sae(Ctx c, const int64_t *stamp) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= c.WH) return;
+    const int64_t s = stamp[q + (int64_t)c.X0 * c.H];
+    SaeCell cell{};
+    cell.tag = s >= 0 ? 0x80000000u : 0u;  // chunk seq 0: never matches a chunk
+    cell.tsnap = s >= 0 ? (uint32_t)s : 0u;
+    c.cells[q] = cell;
+}
+
 // lastEventTime surface for farms_get_last_event_time: stamp of the latest
 // event at each pixel, 0 when never visited (vFlow.cpp:66,264,407).
 __global__ void k_last_time(const SaeCell *cells, int64_t WH, double *out) {
@@ -1568,6 +1613,8 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipMemsetAsync(h->cells, 0, sizeof(SaeCell) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->pcur, 0, sizeof(int32_t) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     return FARMS_OK;
@@ -1953,6 +2000,51 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
     (void)hipFree(d);
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
+    return FARMS_OK;
+}
+
+extern "C" int farms_last_stamps(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
+                                 int64_t n, int64_t n_head, int64_t *d_head, int64_t *d_full) {
+    if (!h || !d_full || (n_head > 0 && !d_head)) return fail(FARMS_EINVAL, "null argument");
+    if (n < 0 || n >= INT_MAX || n_head < 0 || n_head > n) return fail(FARMS_EINVAL, "event count out of range");
+    if (n > 0 && (!d_x || !d_y || !d_t)) return fail(FARMS_EINVAL, "null array");
+    HIPCHK(hipSetDevice(h->prm.device));
+    const int64_t WHs = (int64_t)h->W * h->H;
+    hipStream_t s = h->stream;
+    int32_t *last = nullptr;
+    HIPCHK(hipMallocAsync((void **)&last, sizeof(int32_t) * WHs, s));
+    HIPCHK(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * WHs, s));  // -1: no event
+    if (n_head > 0)
+        hipLaunchKernelGGL(k_last_index, dim3(ceil_div(n_head, 256)), dim3(256), 0, s, d_x, d_y, 0, (int)n_head, h->W, h->H, last);
+    if (d_head) hipLaunchKernelGGL(k_last_stamp, dim3(ceil_div(WHs, 256)), dim3(256), 0, s, last, d_t, WHs, d_head);
+    if (n > n_head)
+        hipLaunchKernelGGL(k_last_index, dim3(ceil_div(n - n_head, 256)), dim3(256), 0, s, d_x, d_y, (int)n_head, (int)n,
+                           h->W, h->H, last);
+    hipLaunchKernelGGL(k_last_stamp, dim3(ceil_div(WHs, 256)), dim3(256), 0, s, last, d_t, WHs, d_full);
+    HIPCHK(hipFreeAsync(last, s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    return FARMS_OK;
+}
+
+extern "C" int farms_merge_stamps(farms_handle *h, const int64_t *d_in, int32_t count, int64_t *d_out) {
+    if (!h || !d_out || (count > 0 && !d_in) || count < 0) return fail(FARMS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(h->prm.device));
+    const int64_t WHs = (int64_t)h->W * h->H;
+    hipLaunchKernelGGL(k_merge_stamps, dim3(ceil_div(WHs, 256)), dim3(256), 0, h->stream, d_in, count, WHs, d_out);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipGetLastError());
+    return FARMS_OK;
+}
+
+extern "C" int farms_seed_sae(farms_handle *h, const int64_t *d_stamp) {
+    if (!h || !d_stamp) return fail(FARMS_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(h->prm.device));
+    Ctx c{};
+    c.W = h->W; c.H = h->H; c.WH = h->WH; c.X0 = h->X0; c.cells = h->cells;
+    hipLaunchKernelGGL(k_seed_sae, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, c, d_stamp);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipGetLastError());
     return FARMS_OK;
 }
 

@@ -107,7 +107,8 @@ class SynthParams(ctypes.Structure):
 HIP_SYMBOLS = (
     "farms_default_params", "farms_create", "farms_destroy", "farms_reset", "farms_process",
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
-    "farms_get_last_event_time", "farms_last_error",
+    "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
+    "farms_seed_sae",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text")
 
@@ -342,6 +343,26 @@ class FlowManager:
 
     def process_events(self, ev: Events) -> Records:
         return self.process(*ev.relative())
+
+    # ---- temporal segments (segments.py); device int64 tensors
+    def last_stamps(self, x, y, t_rel, n_head: int, head, full) -> None:
+        """Per-pixel last stamp (x-major W x H, -1 = none) over the device events
+        [0, n_head) into `head` and over all of them into `full`."""
+        n = int(x.shape[0])
+        _check(self._lib, self._lib.farms_last_stamps(
+            self._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+            ctypes.c_void_p(t_rel.data_ptr()), ctypes.c_int64(n), ctypes.c_int64(int(n_head)),
+            ctypes.c_void_p(head.data_ptr() if head is not None else 0), ctypes.c_void_p(full.data_ptr())))
+
+    def merge_stamps(self, stack, out) -> None:
+        """out = in-order merge of the rows of `stack` (count x W*H, contiguous)."""
+        _check(self._lib, self._lib.farms_merge_stamps(self._h, ctypes.c_void_p(stack.data_ptr()),
+                                                       ctypes.c_int32(int(stack.shape[0])),
+                                                       ctypes.c_void_p(out.data_ptr())))
+
+    def seed_sae(self, stamp) -> None:
+        """Start this (fresh or reset) handle from the SAE surface `stamp`."""
+        _check(self._lib, self._lib.farms_seed_sae(self._h, ctypes.c_void_p(stamp.data_ptr())))
 
     def process_device(self, x, y, t_rel, p, out: dict) -> None:
         """Device-resident variant: torch tensors (int32 x/y/p, int32 view of the

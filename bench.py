@@ -8,11 +8,14 @@ A step = one full pass of the hot path (surfaces reset + every event through
 local fit and multiscale pooling) over the whole resident stream.
 
 Multi-GPU (torchrun, one process per GPU): weak scaling — the stream holds N x
-the per-GPU event count on the same sensor; rank r owns the events of one
-x-strip (event-count quantiles) and its handle stores the strip widened by the
-pooling + fit halo, so its records are bitwise those of a one-GPU run.  No
-data-path collective (strips.py); value = owned events of all
-ranks / max-over-ranks time.
+the per-GPU event count on the same sensor.  On a time-ordered stream (the
+synthetic one is) rank r owns the r-th temporal segment: every step the ranks
+compute their per-pixel last-stamp surfaces on the GPU, all-gather them over
+RCCL, and each rank starts from the merged SAE plus a re-fitted 500 us warm-up
+(segments.py).  --split strips (or an unordered stream) uses
+x-strips with recomputed halos instead (strips.py).  Either way the owned
+records are bitwise those of a one-GPU run; value = owned events of all ranks
+/ max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -31,6 +34,7 @@ sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 
 import farms  # noqa: E402
+import segments  # noqa: E402
 import strips  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
@@ -49,16 +53,17 @@ def parse():
     ap.add_argument("--pool-chunk", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", choices=("segments", "strips"), default="segments",
+                    help="N > 1: temporal segments (time-ordered streams) or x-strips")
     return ap.parse_args()
 
 
-def cpu_baseline(ev, width, height, fs, jump, maxw, n_sample):
-    """Oracle ("port": single-thread C restatement, -O2) on the first n_sample
-    events of the same stream."""
+def cpu_baseline(sample, width, height, fs, jump, maxw):
+    """Oracle ("port": single-thread C restatement, -O2) on a head sample of the
+    same stream."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import OracleFlow
 
-    sample = ev.head(min(n_sample, len(ev)))
     x, y, t, p = sample.relative()
     of = OracleFlow(height, width, fs, 5, jump, maxw)
     t0 = time.perf_counter()
@@ -113,12 +118,35 @@ def main():
     sp.n_events = per_gpu * world  # weak scaling: fixed events per GPU
     ev = farms.synth_generate(sp)  # same seed on every rank: the same stream
     x, y, t, p = ev.relative()
-    strip = strips.plan(x, W, world, fs, maxw)[rank]
-    if world > 1:
+    cpu_sample = ev.head(min(args.cpu_sample, len(ev))) if world == 1 and not args.no_cpu_baseline else None
+    del ev
+    # N > 1: temporal segments on a time-ordered stream, x-strips
+    # otherwise (or with --split strips)
+    split = "none" if world == 1 else args.split
+    if split == "segments" and not segments.is_time_ordered(t):
+        split = "strips"
+    region, owned, seg = None, None, None
+    if split == "segments":
+        segs = segments.plan(t, world)
+        seg = segs[rank]
+        n_head = segments.head_length(segs, rank)
+        sl = slice(seg.warm, seg.end)
+        x, y, t, p = x[sl], y[sl], t[sl], p[sl]
+        n_owned = seg.end - seg.start
+        label = (f"{world} temporal segments of the time-ordered stream: per step the ranks' last-stamp "
+                 f"surfaces are all-gathered over {backend.upper()} and each rank starts from the merged SAE "
+                 f"plus a re-fitted 500 us warm-up ({seg.n_warm} events on rank {rank})")
+    elif split == "strips":
+        strip = strips.plan(x, W, world, fs, maxw)[rank]
         m = strips.region_mask(x, strip)
         x, y, t, p = x[m], y[m], t[m], p[m]
+        region, owned = (strip.reg_lo, strip.reg_hi), (strip.own_lo, strip.own_hi)
+        n_owned = int(strips.owned_mask(x, strip).sum())
+        label = f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, no data-path collective"
+    else:
+        n_owned = len(x)
+        label = "1 GPU"
     n = len(x)
-    n_owned = int(strips.owned_mask(x, strip).sum())
     dx = torch.from_numpy(x).to(dev)
     dy = torch.from_numpy(y).to(dev)
     dt_ = torch.from_numpy(t.view(np.int32)).to(dev)
@@ -126,12 +154,27 @@ def main():
     out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
            for c in farms.COLUMNS[4:]}
     fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk,
-                           region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi))
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=region, owned=owned)
+    if seg is not None:  # stamp surfaces: this rank's [head, full], everyone's, the merged SAE
+        WHs = W * H
+        mine = torch.empty((2, WHs), dtype=torch.int64, device=dev)
+        gath = torch.empty((2 * world, WHs), dtype=torch.int64, device=red_dev)
+        rows = torch.tensor(segments.merge_rows(rank), dtype=torch.int64, device=dev)
+        sel = torch.empty((len(segments.merge_rows(rank)), WHs), dtype=torch.int64, device=dev)
+        sae = torch.empty(WHs, dtype=torch.int64, device=dev)
+        o = seg.n_warm  # the segment's own events start after the warm-up
     torch.cuda.synchronize()
 
     def step():
         fm.reset()
+        if seg is not None:
+            fm.last_stamps(dx[o:], dy[o:], dt_[o:], n_head, mine[0], mine[1])
+            dist.all_gather_into_tensor(gath, mine if red_dev == dev else mine.cpu())
+            if rank > 0:
+                torch.index_select(gath.to(dev, non_blocking=False), 0, rows, out=sel)
+                torch.cuda.synchronize()
+                fm.merge_stamps(sel, sae)
+                fm.seed_sae(sae)
         fm.process_device(dx, dy, dt_, dp, out)
 
     for _ in range(args.warmup):
@@ -184,8 +227,7 @@ def main():
         "config": {"workload": f"BASELINE config {cfg}: {W}x{H} synthetic moving-bars stream, "
                                f"{per_gpu} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
                    "events_per_gpu": per_gpu, "width": W, "height": H, "filtersize": fs,
-                   "parallelism": (f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, "
-                                   "no data-path collective") if world > 1 else "1 GPU"},
+                   "parallelism": label},
         "roofline": roofline,
         "detail": {"valid_frac": round(st["n_valid"] / max(st["n_events"], 1), 4),
                    "ms_prep": round(ts["ms_prep"], 3), "ms_fit_sweep": round(ts["ms_fit"], 3),
@@ -196,7 +238,7 @@ def main():
                    "contrib_per_valid": round(st["pool_contributors"] / max(st["n_valid"], 1), 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(ev, W, H, fs, jump, maxw, args.cpu_sample)
+        line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
     if world > 1:
         line["detail"]["rank0_stored_events"] = n
         line["detail"]["rank0_owned_events"] = n_owned

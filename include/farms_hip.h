@@ -125,6 +125,24 @@ int farms_get_stats(const farms_handle *h, farms_stats *out);
  * reference exposes it as returnFlowTime() (vFlow.h:107). */
 int farms_get_last_event_time(const farms_handle *h, double *out);
 
+/* Temporal segments (multi-GPU on a time-ordered stream).  A
+ * segment of the stream can be processed on its own, with results bitwise
+ * those of the whole run, from (a) the SAE as of its first event and (b) the
+ * local flows of the events of the last 500 us before it (re-fitted as a
+ * warm-up prefix of the segment).  Stamp surfaces are x-major W x H int64
+ * device arrays, -1 = pixel never visited.  Not in the reference (single
+ * process); they feed an RCCL all-gather in bench.py. */
+
+/* Last stamp per pixel over device events [0, n_head) -> d_head (may be NULL
+ * when n_head = 0) and over [0, n) -> d_full. */
+int farms_last_stamps(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t_rel,
+                      int64_t n, int64_t n_head, int64_t *d_head, int64_t *d_full);
+/* d_out[q] = the value of the last of the count arrays d_in[i * W * H + q]
+ * that visited q (i.e. the SAE after the segments in order). */
+int farms_merge_stamps(farms_handle *h, const int64_t *d_in, int32_t count, int64_t *d_out);
+/* Start the handle (fresh or reset) from the SAE d_stamp; flow state stays empty. */
+int farms_seed_sae(farms_handle *h, const int64_t *d_stamp);
+
 /* Number of pooling scales, floor(max_window / window_jump) + 1. */
 int farms_num_scales(const farms_handle *h);
 

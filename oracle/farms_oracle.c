@@ -94,6 +94,22 @@ void farms_oracle_destroy(farms_oracle *o)
 
 int farms_oracle_num_scales(const farms_oracle *o) { return o ? o->nscales : 0; }
 
+/* SAE seed for temporal-segment tests: a visited cell holds Event(x, y, p, t)
+ * and lastEventTime t (vFlow.cpp:264,267), an unvisited one Event(0,0,0,0). */
+void farms_oracle_seed_sae(farms_oracle *o, const int64_t *stamp)
+{
+    const int W = o->W, H = o->H;
+    for (int x = 0; x < W; ++x)
+        for (int y = 0; y < H; ++y) {
+            const size_t c = (size_t)x * H + y;
+            const int vis = stamp[c] >= 0;
+            o->cs_x[c] = vis ? x : 0;
+            o->cs_y[c] = vis ? y : 0;
+            o->cs_t[c] = vis ? (double)stamp[c] : 0.0;
+            o->last_time[c] = vis ? (double)stamp[c] : 0.0;
+        }
+}
+
 /* ---- Eigen 3.4 restatements ------------------------------------------------ */
 
 /* AtA.determinant() on a MatrixXd (vFlow.cpp:1316).  A dynamic-size matrix goes

@@ -33,6 +33,8 @@ def load() -> ctypes.CDLL:
         lib.farms_oracle_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_void_p]
         lib.farms_oracle_destroy.argtypes = [ctypes.c_void_p]
         lib.farms_oracle_num_scales.argtypes = [ctypes.c_void_p]
+        lib.farms_oracle_seed_sae.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        lib.farms_oracle_seed_sae.restype = None
         _lib = lib
     return _lib
 
@@ -59,6 +61,11 @@ class OracleFlow:
             self.close()
         except Exception:
             pass
+
+    def seed_sae(self, stamp) -> None:
+        """Start from an x-major W x H SAE stamp surface (-1: never visited)."""
+        stamp = np.ascontiguousarray(stamp, np.int64)
+        self._lib.farms_oracle_seed_sae(self._h, ctypes.c_void_p(stamp.ctypes.data))
 
     def process(self, x, y, t_rel, p):
         """Returns a dict of the 11 output columns."""

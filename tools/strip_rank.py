@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""One rank of an N-strip weak-scaling run, on one GPU (tuning aid).
+
+Generates the N x E-event stream bench.py --gpus N would generate, plans the
+x-strips exactly as bench.py does, and times the step of the requested ranks
+(their stored region, owned columns) one after the other on device 0.  The
+N-GPU bench value is then predicted as N x E / max-over-ranks step time; the
+driver's own N-GPU run is the measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "aperture-robust-multiscale-optical-flow_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import farms  # noqa: E402
+import strips  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=8, help="strips (simulated GPUs)")
+ap.add_argument("--ranks", default="", help="comma list; default: all")
+ap.add_argument("--events", type=int, default=50_000_000, help="events per GPU")
+ap.add_argument("--fit", default="0")
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+
+W, H, fs, maxw, jump = 1280, 720, 5, 50, 5
+sp = farms.synth_params(3)
+sp.n_events = a.events * a.n
+t0 = time.time()
+ev = farms.synth_generate(sp)
+x, y, t, p = ev.relative()
+del ev
+print(f"synth {len(x)} events in {time.time() - t0:.1f} s", flush=True)
+plan = strips.plan(x, W, a.n, fs, maxw)
+ranks = [int(r) for r in a.ranks.split(",")] if a.ranks else range(a.n)
+dev = torch.device("cuda", 0)
+for fc in [int(v) for v in a.fit.split(",")]:
+    worst = 0.0
+    for r in ranks:
+        s = plan[r]
+        m = strips.region_mask(x, s)
+        dx = torch.from_numpy(x[m]).to(dev)
+        dy = torch.from_numpy(y[m]).to(dev)
+        dt = torch.from_numpy(t[m].view(np.int32)).to(dev)
+        dp = torch.from_numpy(p[m]).to(dev)
+        n = len(dx)
+        owned = int(strips.owned_mask(x[m], s).sum())
+        out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+               for c in farms.COLUMNS[4:]}
+        fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, fit_chunk=fc,
+                               region=(s.reg_lo, s.reg_hi), owned=(s.own_lo, s.own_hi))
+        fm.process_device(dx, dy, dt, dp, out)  # warmup
+        best = 1e9
+        for _ in range(a.reps):
+            fm.reset()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            fm.process_device(dx, dy, dt, dp, out)
+            best = min(best, time.perf_counter() - t1)
+        fm.set_profiling(farms.PROF_TIMING)
+        fm.reset()
+        fm.process_device(dx, dy, dt, dp, out)
+        st = fm.stats()
+        fm.close()
+        worst = max(worst, best)
+        print(json.dumps({"n": a.n, "rank": r, "fit_chunk": fc, "cols": [s.own_lo, s.own_hi], "stored": n,
+                          "owned": owned, "ms": round(best * 1e3, 1), "ms_fit_sweep": round(st["ms_fit"], 1),
+                          "ms_pool_sweep": round(st["ms_pool"], 1), "ms_fit_k": round(st["ms_fit_kernel"], 1),
+                          "ms_pool_k": round(st["ms_pool_kernel"], 1)}), flush=True)
+        del dx, dy, dt, dp, out
+        torch.cuda.empty_cache()
+    print(json.dumps({"n": a.n, "fit_chunk": fc, "predicted_Mev_s": round(a.n * a.events / worst / 1e6, 1),
+                      "worst_ms": round(worst * 1e3, 1)}), flush=True)

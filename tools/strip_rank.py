@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""One rank of an N-strip weak-scaling run, on one GPU (tuning aid).
+"""One rank of an N-rank weak-scaling run, on one GPU (tuning aid).
 
-Generates the N x E-event stream bench.py --gpus N would generate, plans the
-x-strips exactly as bench.py does, and times the step of the requested ranks
-(their stored region, owned columns) one after the other on device 0.  The
-N-GPU bench value is then predicted as N x E / max-over-ranks step time; the
-driver's own N-GPU run is the measurement.
+Generates the N x E-event stream bench.py --gpus N would generate, splits it
+exactly as bench.py does (--split strips: x-strips; segments: temporal
+segments) and times the step of the requested ranks one after the other on
+device 0.  For segments the step is last_stamps + merge + seed + the warm-up
+and segment; the RCCL all-gather itself (2 x 7.4 MB per rank) is not timed.
+The N-GPU bench value is then predicted as N x E / max-over-ranks step time;
+the driver's own N-GPU run is the measurement.
 """
 import argparse
 import json
@@ -19,6 +21,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import farms  # noqa: E402
+import segments  # noqa: E402
 import strips  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -27,6 +30,7 @@ ap.add_argument("--ranks", default="", help="comma list; default: all")
 ap.add_argument("--events", type=int, default=50_000_000, help="events per GPU")
 ap.add_argument("--fit", default="0")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--split", choices=("strips", "segments"), default="strips")
 a = ap.parse_args()
 
 W, H, fs, maxw, jump = 1280, 720, 5, 50, 5
@@ -37,39 +41,59 @@ ev = farms.synth_generate(sp)
 x, y, t, p = ev.relative()
 del ev
 print(f"synth {len(x)} events in {time.time() - t0:.1f} s", flush=True)
-plan = strips.plan(x, W, a.n, fs, maxw)
+plan = strips.plan(x, W, a.n, fs, maxw) if a.split == "strips" else segments.plan(t, a.n)
 ranks = [int(r) for r in a.ranks.split(",")] if a.ranks else range(a.n)
 dev = torch.device("cuda", 0)
 for fc in [int(v) for v in a.fit.split(",")]:
     worst = 0.0
     for r in ranks:
         s = plan[r]
-        m = strips.region_mask(x, s)
+        if a.split == "strips":
+            m = strips.region_mask(x, s)
+            owned = int(strips.owned_mask(x[m], s).sum())
+            region, own, cols = (s.reg_lo, s.reg_hi), (s.own_lo, s.own_hi), [s.own_lo, s.own_hi]
+        else:
+            m = slice(s.warm, s.end)
+            owned = s.end - s.start
+            region, own, cols = None, None, [s.start, s.end]
         dx = torch.from_numpy(x[m]).to(dev)
         dy = torch.from_numpy(y[m]).to(dev)
         dt = torch.from_numpy(t[m].view(np.int32)).to(dev)
         dp = torch.from_numpy(p[m]).to(dev)
         n = len(dx)
-        owned = int(strips.owned_mask(x[m], s).sum())
         out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
                for c in farms.COLUMNS[4:]}
         fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, fit_chunk=fc,
-                               region=(s.reg_lo, s.reg_hi), owned=(s.own_lo, s.own_hi))
-        fm.process_device(dx, dy, dt, dp, out)  # warmup
+                               region=region, owned=own)
+        if a.split == "segments":  # the surfaces of the ranks before this one: stand-ins of the right shape
+            mine = torch.empty((2, W * H), dtype=torch.int64, device=dev)
+            rows = max(len(segments.merge_rows(r)), 1)
+            stack = torch.full((rows, W * H), -1, dtype=torch.int64, device=dev)
+            sae = torch.empty(W * H, dtype=torch.int64, device=dev)
+            o, n_head = s.n_warm, segments.head_length(plan, r)
+
+        def run():
+            if a.split == "segments":
+                fm.last_stamps(dx[o:], dy[o:], dt[o:], n_head, mine[0], mine[1])
+                if r > 0:
+                    fm.merge_stamps(stack, sae)
+                    fm.seed_sae(sae)
+            fm.process_device(dx, dy, dt, dp, out)
+        run()  # warmup
         best = 1e9
         for _ in range(a.reps):
             fm.reset()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            fm.process_device(dx, dy, dt, dp, out)
+            run()
             best = min(best, time.perf_counter() - t1)
         fm.set_profiling(farms.PROF_TIMING)
         fm.reset()
-        fm.process_device(dx, dy, dt, dp, out)
+        run()
         st = fm.stats()
         fm.close()
         worst = max(worst, best)
-        print(json.dumps({"n": a.n, "rank": r, "fit_chunk": fc, "cols": [s.own_lo, s.own_hi], "stored": n,
+        print(json.dumps({"n": a.n, "rank": r, "fit_chunk": fc, "split": a.split, "range": cols, "stored": n,
                           "owned": owned, "ms": round(best * 1e3, 1), "ms_fit_sweep": round(st["ms_fit"], 1),
                           "ms_pool_sweep": round(st["ms_pool"], 1), "ms_fit_k": round(st["ms_fit_kernel"], 1),
                           "ms_pool_k": round(st["ms_pool_kernel"], 1)}), flush=True)

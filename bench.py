@@ -67,10 +67,28 @@ def cpu_baseline(sample, width, height, fs, jump, maxw):
     x, y, t, p = sample.relative()
     of = OracleFlow(height, width, fs, 5, jump, maxw)
     t0 = time.perf_counter()
-    of.process(x, y, t, p)
+    ref = of.process(x, y, t, p)
     dt = time.perf_counter() - t0
-    return {"value": len(sample) / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
+    return ref, {"value": len(sample) / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
             "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, {dt:.1f} s"}
+
+
+def parity_vs_cpu(ref, out, k):
+    """The metric's "max |dtheta| vs CPU ref": the GPU records of the timed run's
+    first k events against the oracle's records of the same k events (the path
+    is causal, so the prefix of a full run equals a run of the prefix).  Bar as
+    in tests/parity.py: validity bit-exact, r within 1e-4 relative, theta within
+    1e-4 rad."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import compare
+
+    gpu = {c: ref[c] for c in farms.COLUMNS[:4]}  # x/y/t/p are inputs, not outputs of process_device
+    gpu.update({c: out[c][:k].cpu().numpy() for c in farms.COLUMNS[4:]})
+    rep = compare(gpu, ref)
+    return {"events_compared": k, "valid_events": rep["valid_ref"], "valid_mismatch": rep["valid_mismatch"],
+            "max_dtheta_true_rad": rep["theta_true_max_abs"], "max_dtheta_local_rad": rep["theta_local_max_abs"],
+            "max_rel_r_true": rep["r_true_max_rel"], "max_rel_r_local": rep["r_local_max_rel"],
+            "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"]}
 
 
 def pmc_traffic(cfg, world, pool_launches):
@@ -238,7 +256,8 @@ def main():
                    "contrib_per_valid": round(st["pool_contributors"] / max(st["n_valid"], 1), 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
+        ref, line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
+        line["parity"] = parity_vs_cpu(ref, out, len(cpu_sample))
     if world > 1:
         line["detail"]["rank0_stored_events"] = n
         line["detail"]["rank0_owned_events"] = n_owned

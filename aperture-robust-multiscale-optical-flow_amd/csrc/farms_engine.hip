@@ -870,7 +870,7 @@ __device__ __forceinline__ double xch(double v) {
     return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
 }
 
-constexpr int kGroupCells = 1024;  // cells per candidate group (16 bitmap words)
+constexpr int kGroupCells = 256;  // cells per candidate group = one k_chain wavefront (4 bitmap words)
 
 
 // Candidate index (in buffer b) of the first candidate with cell index >= L
@@ -888,140 +888,151 @@ __device__ __forceinline__ uint32_t cand_hi(const Ctx &c, int b, int64_t L) {
 }
 
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling
-// chunks [ch0, ch1)).  A block owns one candidate group (kGroupCells = 1024
-// cells = 16 bitmap words; the group's candidates of a chunk take slots
-// [g * 1024, ...) of the chunk's ring buffer, so word offsets need no global
-// scan); wave wv owns words wv, wv + 4, wv + 8, wv + 12, lane = cell.  Each
+// chunks [ch0, ch1)).  A wavefront owns one candidate group (kGroupCells = 256
+// cells = 4 bitmap words, lane = cell of each word); the group's candidates of
+// a chunk take slots [g * 256, ...) of the chunk's ring buffer, so the word
+// offsets are a scalar prefix of the wave's 4 ballots — no block barrier, no
+// global scan, and the waves of a launch never wait for each other.  Each
 // cell's state stays in registers across the chunks: the cursor into its run
-// of P (next event id nxt) and its flow-snapshot stamp ft (-1: snapshot flow
-// invalid).  Per chunk ch (ring buffer ch % NB):
+// of P (next event id nxt), its flow snapshot (snap; ft = its stamp, -1 when
+// the snapshot flow is invalid), and, prefetched one touch ahead, the local
+// flow of the next event at the cell and the run entry after it (pf, pnx), so
+// a chunk's common case (one event at the cell) issues no dependent load.
+// Per chunk ch (ring buffer ch % NB):
 //   bit(q) = q touched in ch, or ft within the kill time of the chunk's stamp
 //            span: a superset of every cell that can contribute to an event
 //            of ch as of that event (vFlow.cpp:1002/1115);
-//   bitmap word + group-local candidate offsets (block scan of 16 counts);
+//   bitmap words + group-local candidate offsets;
 //   fill: candidate record = snapshot flow before ch + first in-chunk flow
 //         and the cell's in-chunk run bounds in P;
-//   advance: snapshot <- last in-chunk event at q, cursor past the chunk.
-// Only cells touched in a chunk or carrying a candidate do memory work; the
-// state round-trips memory once per launch.
-__global__ __launch_bounds__(256) void k_chain(Ctx c, int ch0, int ch1) {
-    __shared__ uint32_t s_cnt[2][16];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t g = blockIdx.x;
+//   advance: snapshot <- last in-chunk event at q, cursor past the chunk,
+//            prefetch of the next touch (events of the super-chunk only: the
+//            fit of later events may still be running).
+// The state round-trips memory once per launch (only cells touched in it).
+constexpr int kChainCells = kGroupCells / 64;  // cells per lane
+struct ChainFlow {  // FlowCell without its padding: L, L cos, L sin, stamp
+    double L, Lc, Ls;
+    uint32_t t;
+};
+__device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
+    const FlowCell f = *p;
+    return ChainFlow{f.L, f.Lc, f.Ls, f.t};
+}
+__global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= c.nblk) return;
     const int n = c.n, C2 = c.C2;
+    const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
     const uint64_t lt = (1ull << lane) - 1;
-    int k[4], kend[4], nxt[4];
-    int64_t ft[4];
-    bool dirty[4], bit[4];
+    int k[kChainCells], kend[kChainCells], nxt[kChainCells], pnx[kChainCells];
+    ChainFlow snap[kChainCells], pf[kChainCells];
+    uint32_t dirty = 0;
+    auto prefetch = [&](int i) {  // the next touch of cell i: its flow and the run entry after it
+        pnx[i] = INT_MAX;
+        pf[i] = ChainFlow{0.0, 0.0, 0.0, 0u};
+        if (nxt[i] < lim) {
+            pf[i] = chain_load(&c.evf[nxt[i]]);
+            if (k[i] + 1 <= kend[i]) pnx[i] = c.P[k[i] + 1];
+        }
+    };
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t q = (g * 16 + wv + 4 * i) * 64 + lane;
-        k[i] = 0; kend[i] = -1; ft[i] = -1;
+    for (int i = 0; i < kChainCells; ++i) {
+        const int64_t q = (g * kChainCells + i) * 64 + lane;
+        k[i] = 0; kend[i] = -1;
+        int64_t ft = -1;
         if (q < c.WH) {
             kend[i] = c.pend[q];
             if (kend[i] >= 0) k[i] = c.pcur[q];  // pcur is only defined for cells with events in this call
-            ft[i] = c.ftime[q];
+            ft = c.ftime[q];
         }
         nxt[i] = k[i] <= kend[i] ? c.P[k[i]] : INT_MAX;
-        dirty[i] = false;
+        snap[i] = ChainFlow{0.0, 0.0, 0.0, 0u};  // an invalid snapshot flow is never read (kCandSnapOk clear)
+        if (ft >= 0) snap[i] = chain_load(&c.fsnap[q]);
     }
-    auto mark = [&](int ch) {  // bits of chunk ch from the current state
+#pragma unroll
+    for (int i = 0; i < kChainCells; ++i) prefetch(i);
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const int b = ch % c.NB;
         const int ce = min((ch + 1) * C2, n);
         const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
+        uint64_t bal[kChainCells];
+        uint32_t woff[kChainCells];
+        uint32_t acc = (uint32_t)(g * kGroupCells);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) bit[i] = nxt[i] < ce || (ft[i] >= 0 && ft[i] > lo && ft[i] < hi);
-    };
-    mark(ch0);
-    for (int ch = ch0; ch < ch1; ++ch) {
-        const int b = ch % c.NB, par = (ch - ch0) & 1;
-        const int ce = min((ch + 1) * C2, n);
-        uint64_t bal[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            bal[i] = __ballot(bit[i]);
-            const int64_t w = g * 16 + wv + 4 * i;
-            if (lane == 0) {
-                s_cnt[par][wv + 4 * i] = (uint32_t)__popcll(bal[i]);
-                if (w < c.nwords) c.bm_ring[(int64_t)b * c.nwords + w] = bal[i];
+        for (int i = 0; i < kChainCells; ++i) {
+            const int64_t ts = (int64_t)snap[i].t;
+            const bool bit = nxt[i] < ce || (snap[i].L > 0 && ts > lo && ts < hi);
+            bal[i] = __ballot(bit);
+            woff[i] = acc;
+            acc += (uint32_t)__popcll(bal[i]);
+            const int64_t w = g * kChainCells + i;
+            if (lane == 0 && w < c.nwords) {
+                c.bm_ring[(int64_t)b * c.nwords + w] = bal[i];
+                c.wo_ring[(int64_t)b * (c.nwords + 1) + w] = woff[i];
             }
         }
-        // block barrier for the word counts in LDS only: the global stores of
-        // this chunk are read by later kernels, not by other waves here
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        // exclusive prefix of the group's 16 word counts
-        const uint32_t cw = lane < 16 ? s_cnt[par][lane] : 0u;
-        uint32_t incl = cw;
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, off, 64);
-            if (lane >= off) incl += v;
-        }
-        const uint32_t excl = incl - cw;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t w = g * 16 + wv + 4 * i;
-            const int64_t q = w * 64 + lane;
-            const uint32_t woff = (uint32_t)(g * kGroupCells) + (uint32_t)__builtin_amdgcn_readlane((int)excl, wv + 4 * i);
-            if (lane == 0 && w < c.nwords) c.wo_ring[(int64_t)b * (c.nwords + 1) + w] = woff;
-            // the loads of the common case (one event at q in the chunk) are
-            // issued together: the run's next id, the first in-chunk flow, the
-            // old snapshot; a longer run is walked afterwards
+        for (int i = 0; i < kChainCells; ++i) {
+            const int64_t q = (g * kChainCells + i) * 64 + lane;
             const bool touched = nxt[i] < ce;
             const int k1 = k[i];
             const int e1 = touched ? nxt[i] : INT_MAX;
-            int nx = INT_MAX;
-            FlowCell f1{}, snap{};
-            if (touched) {
-                if (k1 + 1 <= kend[i]) nx = c.P[k1 + 1];
-                f1 = c.evf[e1];
-            }
-            if (bit[i]) snap = c.fsnap[q];
-            FlowCell fl = f1;  // flow of the last in-chunk event at q
-            if (touched) {
-                int kk = k1 + 1, last = e1, nn = nx;
-                while (nn < ce) {
-                    last = nn;
-                    ++kk;
-                    nn = kk <= kend[i] ? c.P[kk] : INT_MAX;
+            if ((bal[i] >> lane) & 1) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
+                int run_hi = k1;
+                if (touched) {  // the run's last in-chunk position (a longer run is rare)
+                    int nn = pnx[i];
+                    while (nn < ce) {
+                        ++run_hi;
+                        nn = run_hi + 1 <= kend[i] ? c.P[run_hi + 1] : INT_MAX;
+                    }
                 }
-                if (last != e1) fl = c.evf[last];
-                k[i] = kk;
-                nxt[i] = nn;
-            }
-            if (bit[i]) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
                 CandHdr hd;
                 CandVal v;
-                hd.lin = (uint32_t)q | (snap.L > 0 ? kCandSnapOk : 0u);
-                hd.t_snap = snap.t;
-                v.L_snap = snap.L; v.Lc_snap = snap.Lc; v.Ls_snap = snap.Ls;
+                hd.lin = (uint32_t)q | (snap[i].L > 0 ? kCandSnapOk : 0u);
+                hd.t_snap = snap[i].t;
+                v.L_snap = snap[i].L; v.Lc_snap = snap[i].Lc; v.Ls_snap = snap[i].Ls;
                 if (touched) {
                     hd.e1 = e1;
-                    hd.lin |= (k[i] - 1 > k1 ? kCandMore : 0u) | (f1.L > 0 ? kCandOneOk : 0u);
-                    hd.t1 = f1.t;
-                    v.L1 = f1.L; v.Lc1 = f1.Lc; v.Ls1 = f1.Ls;
-                    v.run_lo = k1; v.run_hi = k[i] - 1;
+                    hd.lin |= (run_hi > k1 ? kCandMore : 0u) | (pf[i].L > 0 ? kCandOneOk : 0u);
+                    hd.t1 = pf[i].t;
+                    v.L1 = pf[i].L; v.Lc1 = pf[i].Lc; v.Ls1 = pf[i].Ls;
+                    v.run_lo = k1; v.run_hi = run_hi;
                 } else {
                     hd.e1 = INT_MAX;
                     hd.t1 = 0;
                     v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
                     v.run_lo = 0; v.run_hi = 0;
                 }
-                const int64_t kb = (int64_t)b * c.cstride + woff + (uint32_t)__popcll(bal[i] & lt);
+                const int64_t kb = (int64_t)b * c.cstride + woff[i] + (uint32_t)__popcll(bal[i] & lt);
                 c.hdr_ring[kb] = hd;
                 c.val_ring[kb] = v;
             }
-            if (touched) {  // snapshot <- last event of the chunk at q
-                c.fsnap[q] = fl;
-                ft[i] = fl.L > 0 ? (int64_t)fl.t : -1;
-                dirty[i] = true;
+            if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
+                int kk = k1 + 1, last = e1, nn = pnx[i];
+                while (nn < ce) {
+                    last = nn;
+                    ++kk;
+                    nn = kk <= kend[i] ? c.P[kk] : INT_MAX;
+                }
+                snap[i] = last != e1 ? chain_load(&c.evf[last]) : pf[i];
+                k[i] = kk;
+                nxt[i] = nn;
+                dirty |= 1u << i;
+                prefetch(i);
             }
         }
-        if (ch + 1 < ch1) mark(ch + 1);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t q = (g * 16 + wv + 4 * i) * 64 + lane;
-        if (dirty[i]) { c.ftime[q] = ft[i]; c.pcur[q] = k[i]; }
+    for (int i = 0; i < kChainCells; ++i) {
+        const int64_t q = (g * kChainCells + i) * 64 + lane;
+        if ((dirty >> i) & 1) {
+            FlowCell f;
+            f.L = snap[i].L; f.Lc = snap[i].Lc; f.Ls = snap[i].Ls; f.t = snap[i].t; f.pad = 0;
+            c.fsnap[q] = f;
+            c.ftime[q] = snap[i].L > 0 ? (int64_t)snap[i].t : -1;
+            c.pcur[q] = k[i];
+        }
     }
 }
 
@@ -1793,7 +1804,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             const int fl = std::min(f, n_fit_chunks - 1);
             if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
-        hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(256), 0, sc, c, ch0, ch1);
+        hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, 4)), dim3(256), 0, sc, c, ch0, ch1);
         HIPCHK(hipEventRecord(ev_cand(S), sc));
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);

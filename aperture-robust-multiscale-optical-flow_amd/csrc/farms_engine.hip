@@ -677,6 +677,226 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
 
 
 // ---------------------------------------------------------------------------
+// Cross-lane exchange with the partner lane l ^ (1 << S): DPP quad
+// permutations for S = 0, 1, ds_swizzle (bitmask mode, 32-lane groups) for
+// S = 2..4, ds_bpermute for S = 5.
+template <int S>
+__device__ __forceinline__ int xch32(int v) {
+    if constexpr (S == 0) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    else if constexpr (S == 1) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    else if constexpr (S == 2) return __builtin_amdgcn_ds_swizzle(v, 0x101F);
+    else if constexpr (S == 3) return __builtin_amdgcn_ds_swizzle(v, 0x201F);
+    else if constexpr (S == 4) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
+    else return __shfl_xor(v, 32, 64);
+}
+template <int S>
+__device__ __forceinline__ double xch(double v) {
+    return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
+}
+
+// ---------------------------------------------------------------------------
+// Quad-cooperative fit (fRad known at compile time): four lanes per event, so
+// a 64k-event fit chunk is 4096 wavefronts and each lane issues a quarter of
+// the dependent column loads.  Lane j of the quad scores union columns
+// du = -2fRad + j, +4, ... and gathers window columns j, j + 4, ...; the
+// integer window scores, the visited mask and the normal-matrix sums are
+// combined with quad DPP exchanges (exact), the inlier count likewise.  The
+// order-sensitive (A2*At)*Y accumulation runs in full on every lane of the
+// quad from the window stamps in LDS, in the reference order, so all four
+// lanes hold the bitwise result of the per-thread path.
+__device__ __forceinline__ int64_t quad_sum_i64(int64_t v) {
+    int hi = (int)(v >> 32), lo = (int)(uint32_t)v;
+    int64_t o = ((int64_t)xch32<0>(hi) << 32) | (uint32_t)xch32<0>(lo);
+    v += o;
+    hi = (int)(v >> 32); lo = (int)(uint32_t)v;
+    o = ((int64_t)xch32<1>(hi) << 32) | (uint32_t)xch32<1>(lo);
+    return v + o;
+}
+__device__ __forceinline__ uint64_t quad_or_u64(uint64_t v) {
+    int hi = (int)(v >> 32), lo = (int)(uint32_t)v;
+    v |= ((uint64_t)(uint32_t)xch32<0>(hi) << 32) | (uint32_t)xch32<0>(lo);
+    hi = (int)(v >> 32); lo = (int)(uint32_t)v;
+    return v | ((uint64_t)(uint32_t)xch32<1>(hi) << 32) | (uint32_t)xch32<1>(lo);
+}
+
+template <int FR>
+__device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq, int j, uint32_t *lt, double &vx_out,
+                                               double &vy_out) {
+    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
+    const int W = c.W, H = c.H;
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t te = c.t[e];
+    vx_out = 0.0;
+    vy_out = 0.0;
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
+        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    if (!any) return;  // uniform over the quad
+    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+        const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
+        const int cbase = (u0 - c.X0) * H + v0;
+#pragma unroll
+        for (int i = 0; i < len; ++i) {
+            const int v = v0 + i;
+            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
+#pragma unroll 1
+    for (int du = -2 * FR + j; du <= 2 * FR; du += 4) {
+        uint4 col[US];
+        load_col(ex + du, ey - 2 * FR, US, col);
+        const int u = ex + du;
+        if (u < 0 || u >= W) continue;
+        int64_t dd[US];
+#pragma unroll
+        for (int i = 0; i < US; ++i) {
+            const int v = ey + i - 2 * FR;
+            dd[i] = 0;
+            if (v < 0 || v >= H) continue;
+            const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+        }
+#pragma unroll
+        for (int ovi = 0; ovi < 3; ++ovi) {
+            int64_t sv = 0;
+#pragma unroll
+            for (int i = ovi * FR; i <= ovi * FR + 2 * FR; ++i) sv += dd[i];
+#pragma unroll
+            for (int oui = 0; oui < 3; ++oui) {
+                const int ou = (oui - 1) * FR;
+                if (du - ou <= FR && ou - du <= FR) score[oui * 3 + ovi] += sv;
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) score[w] = quad_sum_i64(score[w]);
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
+
+    // ---- gather the winning window, cx-major (vFlow.cpp:923-930): this lane's
+    // columns into LDS (lt[k * 64]), visited mask combined over the quad
+    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
+    uint64_t vis = 0;
+#pragma unroll 1
+    for (int cxo = j; cxo < side; cxo += 4) {
+        uint4 col[side];
+        load_col(bi - FR + cxo, bj - FR, side, col);
+        const int u = bi + cxo - FR;
+#pragma unroll
+        for (int cyo = 0; cyo < side; ++cyo) {
+            const int k = cxo * side + cyo;
+            const int64_t st = sae_resolve_h(c, col[cyo], (uint32_t)((u - c.X0) * H + bj - FR + cyo), e, seq);
+            vis |= st >= 0 ? 1ull << k : 0ull;
+            lt[k * 64] = st < 0 ? 0u : (uint32_t)st;
+        }
+    }
+    vis = quad_or_u64(vis);
+    // the window's stamps were written by the other lanes of this wave's quad
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+        const int cx = bi + k / side - FR, cy = bj + k % side - FR;
+        const bool vk = (vis >> k) & 1;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = lt[k * 64];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
+    syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    if (DET < 1) return;  // 0 inliers; uniform over the quad
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < np; ++k) {  // every lane, reference order
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1, m2;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+            m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+            m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+        }
+        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+    }
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+    (void)r2;
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    inliers += xch32<0>(inliers);
+    inliers += xch32<1>(inliers);
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    const double speed = 1.0 / dtdp;
+    const double angle = atan2(r0, r1);
+    vx_out = speed * cos(angle);
+    vy_out = speed * sin(angle);
+}
+
+// Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
+template <int FR>
+__global__ __launch_bounds__(256) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
+    constexpr int NPC = (2 * FR + 1) * (2 * FR + 1);
+    __shared__ uint32_t s_tk[NPC * 64];
+    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2);
+    if (w >= c1) return;  // whole quads
+    const int j = threadIdx.x & 3;
+    const int e = c.Q[w];
+    double vx, vy;
+    fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
+    if (j == 0) fit_store(c, e, vx, vy);
+}
+
+// ---------------------------------------------------------------------------
 // Wave-cooperative fit of one event (any fRad, every lookup complete): the
 // lanes resolve the stamps of the union of the 9 candidate windows into LDS
 // (these lookups are the latency: pixels with many in-chunk events need a run
@@ -852,24 +1072,6 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
     }
 }
 
-// ---------------------------------------------------------------------------
-// Cross-lane exchange with the partner lane l ^ (1 << S): DPP quad
-// permutations for S = 0, 1, ds_swizzle (bitmask mode, 32-lane groups) for
-// S = 2..4, ds_bpermute for S = 5.
-template <int S>
-__device__ __forceinline__ int xch32(int v) {
-    if constexpr (S == 0) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
-    else if constexpr (S == 1) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
-    else if constexpr (S == 2) return __builtin_amdgcn_ds_swizzle(v, 0x101F);
-    else if constexpr (S == 3) return __builtin_amdgcn_ds_swizzle(v, 0x201F);
-    else if constexpr (S == 4) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
-    else return __shfl_xor(v, 32, 64);
-}
-template <int S>
-__device__ __forceinline__ double xch(double v) {
-    return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
-}
-
 constexpr int kGroupCells = 256;  // cells per candidate group = one k_chain wavefront (4 bitmap words)
 
 
@@ -899,9 +1101,11 @@ __device__ __forceinline__ uint32_t cand_hi(const Ctx &c, int b, int64_t L) {
 // flow of the next event at the cell and the run entry after it (pf, pnx), so
 // a chunk's common case (one event at the cell) issues no dependent load.
 // Per chunk ch (ring buffer ch % NB):
-//   bit(q) = q touched in ch, or ft within the kill time of the chunk's stamp
-//            span: a superset of every cell that can contribute to an event
-//            of ch as of that event (vFlow.cpp:1002/1115);
+//   bit(q) = q's snapshot flow is valid and its stamp within the kill time
+//            of the chunk's stamp span, or q's first event in ch has valid
+//            flow, or q fires more than once in ch: a superset of every cell
+//            that can contribute to an event of ch as of that event
+//            (vFlow.cpp:1002/1115);
 //   bitmap words + group-local candidate offsets;
 //   fill: candidate record = snapshot flow before ch + first in-chunk flow
 //         and the cell's in-chunk run bounds in P;
@@ -961,8 +1165,13 @@ __global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
         uint32_t acc = (uint32_t)(g * kGroupCells);
 #pragma unroll
         for (int i = 0; i < kChainCells; ++i) {
+            // a candidate can contribute to some event of the chunk: through its
+            // snapshot (valid flow, stamp within the kill time of the chunk's
+            // span), or through an in-chunk event with valid flow (the first
+            // one, or any of a longer run)
             const int64_t ts = (int64_t)snap[i].t;
-            const bool bit = nxt[i] < ce || (snap[i].L > 0 && ts > lo && ts < hi);
+            const bool bit = (snap[i].L > 0 && ts > lo && ts < hi) ||
+                             (nxt[i] < ce && (pf[i].L > 0 || pnx[i] < ce));
             bal[i] = __ballot(bit);
             woff[i] = acc;
             acc += (uint32_t)__popcll(bal[i]);
@@ -1650,7 +1859,16 @@ pool_launcher pool_for(int K) {
     }
 }
 
-void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s) {
+void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad) {
+    if (quad) {
+        const dim3 g(ceil_div(c1 - c0, 64)), b(256);
+        switch (fr) {
+        case 1: hipLaunchKernelGGL(k_fit_quad<1>, g, b, 0, s, c, c0, c1, seq); return;
+        case 2: hipLaunchKernelGGL(k_fit_quad<2>, g, b, 0, s, c, c0, c1, seq); return;
+        case 3: hipLaunchKernelGGL(k_fit_quad<3>, g, b, 0, s, c, c0, c1, seq); return;
+        default: return;
+        }
+    }
     const dim3 g(ceil_div(c1 - c0, 256)), b(256);
     switch (fr) {
     case 1: hipLaunchKernelGGL(k_fit<1>, g, b, 0, s, c, c0, c1, seq); break;
@@ -1765,6 +1983,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
     pool_launcher pl = pool_for(h->K);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
+    const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
+    const bool fit_quad = !(fq && fq[0] == '0');
     int fit_launches = 0;
     auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
     auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F
@@ -1774,7 +1994,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
                            c1, seq);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * f], s));
         if (fast_fit) {
-            launch_fit(c, h->fr, c0, c1, seq, s);
+            launch_fit(c, h->fr, c0, c1, seq, s, fit_quad);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, c, seq, h->Q + c0, c1 - c0);
         }
@@ -1941,9 +2161,13 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // path: high priority; the bulk pooling launches fill the remaining CUs
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess)
+    // FARMS_STREAM_PRIO = three digits (fit, chain, pool), 1 = high: tuning aid
+    int pr[3] = {prio_hi, prio_hi, prio_lo};
+    if (const char *sp = getenv("FARMS_STREAM_PRIO"))
+        for (int i = 0; i < 3 && sp[i]; ++i) pr[i] = sp[i] == '1' ? prio_hi : prio_lo;
+    if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, pr[0]) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, pr[1]) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, pr[2]) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));

@@ -1476,12 +1476,12 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         else if (kind == 1) { const CandVal &v = cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
         else { const FlowCell fe = c.evf[en.x]; L = fe.L; Lc = fe.Lc; Ls = fe.Ls; }
     };
-    // ---- phase B1: length sum and count per scale; lane l takes a contiguous
-    // share of each staged batch
+    // ---- phase B1: length sum per scale, lane l taking a contiguous share of
+    // each staged batch; contributor count per scale from ballots (scalar)
     constexpr int kShare = kPoolCap / 64;
     double sL[K];
-    int cntk[K];
-    double vL[kShare];  // the lane's staged lengths (last pass)
+    int cntk[K];           // wave-uniform
+    double vL[kShare];     // the lane's staged lengths (last pass)
     int vk0[kShare];
 #pragma unroll
     for (int k = 0; k < K; ++k) { sL[k] = 0.0; cntk[k] = 0; }
@@ -1506,35 +1506,40 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
                 vL[j] = length_of(en);
             }
         }
+        for (int r0 = 0; r0 < nb; r0 += 64) {  // counts: contributor r0 + lane
+            const int k0 = r0 + lane < nb ? (int)(s_con[r0 + lane].y >> 8) : K;
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) cntk[kk] += (int)__popcll(__ballot(k0 <= kk));
+        }
 #pragma unroll
         for (int j = 0; j < kShare; ++j) {
 #pragma unroll
             for (int kk = 0; kk < K; ++kk)
-                if (kk >= vk0[j]) { sL[kk] += vL[j]; cntk[kk] += 1; }
+                if (kk >= vk0[j]) sL[kk] += vL[j];
         }
     }
-    // wave totals: slot 2k = length sum of scale k, slot 2k+1 = its count
-    constexpr int LP = K <= 4 ? 3 : (K <= 8 ? 4 : 5);
+    // wave totals: lane l holds the length sum of scale l mod 2^LP
+    constexpr int LP = K <= 2 ? 1 : (K <= 4 ? 2 : (K <= 8 ? 3 : 4));
     double slot[1 << LP];
 #pragma unroll
-    for (int q = 0; q < (1 << LP); ++q) slot[q] = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) { slot[2 * k] = sL[k]; slot[2 * k + 1] = (double)cntk[k]; }
+    for (int q = 0; q < (1 << LP); ++q) slot[q] = q < K ? sL[q] : 0.0;
     tsum<LP>(slot, lane);
     // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
-    // lane 2k (mod 2^LP) holds scale k's mean; the winner is the lowest k
-    // whose mean equals the maximum, if the maximum is > 0
-    const double mine = slot[0], partner = xch<0>(slot[0]);
+    // the winner is the lowest k whose mean equals the maximum, if it is > 0
     const int sl = lane & ((1 << LP) - 1);
-    const bool is_len = !(sl & 1) && (sl >> 1) < K;
-    const double mean = is_len && partner > 0 ? mine / partner : 0.0;
+    int cnt_sl = 0;
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk) cnt_sl = sl == kk ? cntk[kk] : cnt_sl;
+    const bool is_len = sl < K;
+    const double mean = is_len && cnt_sl > 0 ? slot[0] / (double)cnt_sl : 0.0;
     const double maxv = wave_max(mean);
     int mi = 0, cnt_mi = 0;
     if (maxv > 0) {
         const uint64_t hit = __ballot(is_len && mean == maxv);
         const int lw = __builtin_ctzll(hit);
-        mi = (lw & ((1 << LP) - 1)) >> 1;
-        cnt_mi = (int)__shfl(partner, lw, 64);
+        mi = lw & ((1 << LP) - 1);
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) cnt_mi = mi == kk ? cntk[kk] : cnt_mi;
     }
     // ---- phase B2: mean vector of the winning scale (vFlow.cpp:1067-1075)
     double sXY[2] = {0.0, 0.0};

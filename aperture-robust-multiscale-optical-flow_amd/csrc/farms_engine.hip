@@ -883,8 +883,11 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
 }
 
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
+#ifndef FARMS_FIT_WAVES
+#define FARMS_FIT_WAVES 1  // minimum waves per SIMD requested of the register allocator
+#endif
 template <int FR>
-__global__ __launch_bounds__(256) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
+__global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
     constexpr int NPC = (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * 64];
     const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2);

@@ -195,6 +195,21 @@ __device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uin
     return sae_resolve_h(c, sae_head(c, q), q, e, seq);
 }
 
+// XCD-aware work order: consecutive blocks are dealt round-robin to the 8
+// XCDs (each with its own L2).  Block b instead takes logical block
+// xcd_block(b, G), so that each XCD works through one contiguous range of the
+// (tile-ordered) work and neighbouring events share an L2.  Bijective on [0, G).
+__device__ __forceinline__ int xcd_block(int b, int G) {
+    const int q = G >> 3, r = G & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+#ifndef FARMS_XCD
+#define FARMS_XCD 1  // 0: plain blockIdx order (A/B aid)
+#endif
+__device__ __forceinline__ int work_block() {
+    return FARMS_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
+
 // ---------------------------------------------------------------------------
 // prep
 
@@ -890,6 +905,8 @@ template <int FR>
 __global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
     constexpr int NPC = (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * 64];
+    // (plain block order: an XCD-contiguous split of a 1,024-block fit launch
+    // measured 7% slower, its per-XCD work being uneven)
     const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -1290,6 +1307,25 @@ __device__ __forceinline__ void tsum(double (&v)[N], int lane) {
     tsum_step<0, LP, N>(v, lane);
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
+// 16-lane row, then the row broadcasts of lanes 15 and 31.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = (int)__lane_id(), rl = lane & 15;
+    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    if (rl >= 1) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    if (rl >= 2) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    if (rl >= 4) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    if (rl >= 8) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15
+    if ((lane & 31) >= 16) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xF, 0xF, false);  // row_bcast:31
+    if (lane >= 32) v += t;
+    return v;
+}
+
 // Max over the 64 lanes (exact).
 __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, xch<0>(v));
@@ -1342,11 +1378,15 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // A row's cell range maps to one candidate slice per candidate group it
-    // overlaps (ranges are shorter than a group: at most two segments).
-    int carry = 0, nz = 0;
-    for (int r0 = 0; r0 < nrows; r0 += 64) {
-        const int r = r0 + lane;
-        int a0 = 0, n0 = 0, a1 = 0, n1 = 0;
+    // overlaps (ranges are shorter than a group: at most two segments; the
+    // second starts at its group's first slot, whose index is the group's
+    // first cell index).  Lane l handles rows l and l + 64 (2M+1 <= 127): the
+    // lookups of both are in flight before either is used.
+    int a0[2], n0[2], a1[2], n1[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        const int r = lane + 64 * hh;
+        a0[hh] = 0; n0[hh] = 0; a1[hh] = 0; n1[hh] = 0;
         if (r < nrows) {
             const int base = (i_lo + r) * H;
             int l1 = base + j_hi;
@@ -1357,38 +1397,39 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
             if (l1 > WHl - 1) l1 = WHl - 1;
             if (l0 <= l1) {
                 const int gb = l1 & ~(kGroupCells - 1);  // first cell of l1's group
-                a0 = (int)cand_lo(c, buf, l0);
+                a0[hh] = (int)cand_lo(c, buf, l0);
                 if (l0 < gb) {
-                    n0 = (int)cand_hi(c, buf, gb - 1) - a0;
-                    a1 = (int)cand_lo(c, buf, gb);
-                    n1 = (int)cand_hi(c, buf, l1) - a1;
+                    n0[hh] = (int)cand_hi(c, buf, gb - 1) - a0[hh];
+                    a1[hh] = gb;
+                    n1[hh] = (int)cand_hi(c, buf, l1) - gb;
                 } else {
-                    n0 = (int)cand_hi(c, buf, l1) - a0;
+                    n0[hh] = (int)cand_hi(c, buf, l1) - a0[hh];
                 }
             }
         }
-        const int cnt = n0 + n1;
-        int incl = cnt;  // inclusive wave scan
+    }
+    int carry = 0, nz = 0;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += v;
-        }
+    for (int hh = 0; hh < 2; ++hh) {
+        if (64 * hh >= nrows) break;
+        const int r = lane + 64 * hh;
+        const int cnt = n0[hh] + n1[hh];
+        const int incl = wave_incl_scan(cnt);
         const int start = carry + incl - cnt;
         const uint64_t lt = (1ull << lane) - 1;
-        const uint64_t b0 = __ballot(n0 > 0), b1 = __ballot(n1 > 0);
+        const uint64_t b0 = __ballot(n0[hh] > 0), b1 = __ballot(n1[hh] > 0);
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
-        if (n0 > 0) {
-            s_row[idx++] = make_int2(r, a0 - start);
+        if (n0[hh] > 0) {
+            s_row[idx++] = make_int2(r, a0[hh] - start);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
-        if (n1 > 0) {
-            const int st1 = start + n0;
-            s_row[idx] = make_int2(r, a1 - st1);
+        if (n1[hh] > 0) {
+            const int st1 = start + n0[hh];
+            s_row[idx] = make_int2(r, a1[hh] - st1);
             atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
         }
         nz += (int)__popcll(b0) + (int)__popcll(b1);
-        carry += __shfl(incl, 63, 64);
+        carry += __builtin_amdgcn_readlane(incl, 63);
     }
     // the LDS arrays are private to this wave: a wavefront-scope fence orders
     // the writes above before the reads below
@@ -1608,7 +1649,7 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     __shared__ int2 s_row[4][kPoolRowCap];
     __shared__ uint2 s_con[4][kPoolCap];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int w = c0 + work_block() * 4 + wv;
     if (w >= c1) return;
     const int e = c.Q[w];
     if (!c.valid[e]) return;

@@ -111,9 +111,7 @@ struct CandVal {
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
-constexpr int kPoolMaxM = 63;  // largest maxWindow: window rows 2M+1 <= kPoolRowCap
-constexpr int kPoolRowCap = 256;  // row segments (<= 2 per row)
-constexpr int kPoolBitWords = ((2 * kPoolMaxM + 1) * (2 * kPoolMaxM + 1) + 63) / 64;  // flattened positions
+constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
     int W, H, n;
@@ -147,6 +145,7 @@ struct Ctx {
     CandVal *val_ring;
     int64_t nwords;
     int NB, C2;            // ring size, events per pooling chunk
+    int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // outputs
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
@@ -1367,7 +1366,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     const int WHs = (int)c.WHs;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= kPoolRowCap / 2
+    const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= 127
     // ---- per-row candidate slices: flattened start of each non-empty row as a
     // bit of s_start, and its candidate offset in s_row
     uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
@@ -1645,9 +1644,11 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #endif
 template <int K>
 __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
-    __shared__ uint64_t s_start[4][kPoolBitWords];
-    __shared__ int2 s_row[4][kPoolRowCap];
-    __shared__ uint2 s_con[4][kPoolCap];
+    // LDS per wave, sized for maxWindow M at launch (pool_lds_bytes): segment-
+    // start bitmap over the flattened window, <= 2 row segments per window
+    // row, kPoolCap staged contributors
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
+    const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int w = c0 + work_block() * 4 + wv;
     if (w >= c1) return;
@@ -1656,7 +1657,10 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     const int ex = c.x[e];
     if (ex < c.own_lo || ex >= c.own_hi) return;
     const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    pool_event<K>(c, e, ex, c.y[e], c.t[e], buf, lane, s_start[wv], s_row[wv], s_con[wv]);
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap);
+    int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
+    uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs);
+    pool_event<K>(c, e, ex, c.y[e], c.t[e], buf, lane, s_start, s_row, s_con);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -1892,7 +1896,8 @@ int reset_surfaces(farms_handle *h) {
 template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), 0, s, c, c0, c1);
+    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap);
+    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), lds, s, c, c0, c1);
 }
 
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
@@ -1964,6 +1969,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.bm_ring = h->bm_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
+    c.pool_bw = ((2 * h->M + 1) * (2 * h->M + 1) + 63) / 64;  // flattened window positions
+    c.pool_rs = 2 * (2 * h->M + 1);                             // <= 2 segments per window row
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;

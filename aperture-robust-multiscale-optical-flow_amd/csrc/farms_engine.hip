@@ -896,13 +896,180 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     vy_out = speed * sin(angle);
 }
 
+// Variant that keeps the union: every lane writes the stamps of its union
+// columns to the wave's LDS tile (ut[cell * 64], cell = column * US + row) and
+// their visited bits to a register mask, so the winning window needs no second
+// round of loads (window column cxo is union column (bw / 3) * FR + cxo).
+template <int FR>
+__device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t seq, int j, uint32_t *ut, double &vx_out,
+                                                 double &vy_out) {
+    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
+    const int W = c.W, H = c.H;
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t te = c.t[e];
+    vx_out = 0.0;
+    vy_out = 0.0;
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
+        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    if (!any) return;  // uniform over the quad
+    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+        const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
+        const int cbase = (u0 - c.X0) * H + v0;
+#pragma unroll
+        for (int i = 0; i < len; ++i) {
+            const int v = v0 + i;
+            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
+    uint64_t umask = 0;  // visited bits of this lane's union cells: (slot * US + row), slot = column / 4
+#pragma unroll 1
+    for (int du = -2 * FR + j; du <= 2 * FR; du += 4) {
+        uint4 col[US];
+        load_col(ex + du, ey - 2 * FR, US, col);
+        const int u = ex + du;
+        if (u < 0 || u >= W) continue;
+        const int ucol = du + 2 * FR;  // union column index
+        int64_t dd[US];
+#pragma unroll
+        for (int i = 0; i < US; ++i) {
+            const int v = ey + i - 2 * FR;
+            dd[i] = 0;
+            if (v < 0 || v >= H) continue;
+            const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            ut[(ucol * US + i) * 64] = tk;
+            umask |= st >= 0 ? 1ull << ((ucol >> 2) * US + i) : 0ull;
+            dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+        }
+#pragma unroll
+        for (int ovi = 0; ovi < 3; ++ovi) {
+            int64_t sv = 0;
+#pragma unroll
+            for (int i = ovi * FR; i <= ovi * FR + 2 * FR; ++i) sv += dd[i];
+#pragma unroll
+            for (int oui = 0; oui < 3; ++oui) {
+                const int ou = (oui - 1) * FR;
+                if (du - ou <= FR && ou - du <= FR) score[oui * 3 + ovi] += sv;
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) score[w] = quad_sum_i64(score[w]);
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
+
+    // ---- the winning window, cx-major (vFlow.cpp:923-930), from the union tile:
+    // visited bits of the window cells of this lane's columns, combined over the quad
+    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
+    const int ub = (bw / 3) * FR, vb = (bw % 3) * FR;  // window origin in the union
+    uint64_t vis = 0;
+#pragma unroll
+    for (int cxo = 0; cxo < side; ++cxo) {
+        const int uc = ub + cxo;
+        if ((uc & 3) != j) continue;
+        const uint64_t colbits = (umask >> ((uc >> 2) * US + vb)) & ((1ull << side) - 1);
+        vis |= colbits << (cxo * side);
+    }
+    vis = quad_or_u64(vis);
+    // the union stamps were written by the other lanes of this wave's quad
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+        const int kx = k / side, ky = k % side;
+        const int cx = bi + kx - FR, cy = bj + ky - FR;
+        const bool vk = (vis >> k) & 1;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = ut[((ub + kx) * US + vb + ky) * 64];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
+    syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    if (DET < 1) return;  // 0 inliers; uniform over the quad
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
+    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < np; ++k) {  // every lane, reference order
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1, m2;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+            m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+            m2 = (d2 * X + d5 * Y) + d8 * 1.0;
+        }
+        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
+        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+    }
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
+    (void)r2;
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    inliers += xch32<0>(inliers);
+    inliers += xch32<1>(inliers);
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    const double speed = 1.0 / dtdp;
+    const double angle = atan2(r0, r1);
+    vx_out = speed * cos(angle);
+    vy_out = speed * sin(angle);
+}
+
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
 #ifndef FARMS_FIT_WAVES
 #define FARMS_FIT_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
-template <int FR>
+template <int FR, bool UT>
 __global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
-    constexpr int NPC = (2 * FR + 1) * (2 * FR + 1);
+    constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * 64];
     // (plain block order: an XCD-contiguous split of a 1,024-block fit launch
     // measured 7% slower, its per-XCD work being uneven)
@@ -911,7 +1078,8 @@ __global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0
     const int j = threadIdx.x & 3;
     const int e = c.Q[w];
     double vx, vy;
-    fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
+    if constexpr (UT) fit_event_quad_u<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
+    else fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
     if (j == 0) fit_store(c, e, vx, vy);
 }
 
@@ -1913,13 +2081,19 @@ pool_launcher pool_for(int K) {
     }
 }
 
-void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad) {
+void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile) {
     if (quad) {
         const dim3 g(ceil_div(c1 - c0, 64)), b(256);
         switch (fr) {
-        case 1: hipLaunchKernelGGL(k_fit_quad<1>, g, b, 0, s, c, c0, c1, seq); return;
-        case 2: hipLaunchKernelGGL(k_fit_quad<2>, g, b, 0, s, c, c0, c1, seq); return;
-        case 3: hipLaunchKernelGGL(k_fit_quad<3>, g, b, 0, s, c, c0, c1, seq); return;
+        case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq); return;
+        case 2:
+            if (union_tile) hipLaunchKernelGGL((k_fit_quad<2, true>), g, b, 0, s, c, c0, c1, seq);
+            else hipLaunchKernelGGL((k_fit_quad<2, false>), g, b, 0, s, c, c0, c1, seq);
+            return;
+        case 3:
+            if (union_tile) hipLaunchKernelGGL((k_fit_quad<3, true>), g, b, 0, s, c, c0, c1, seq);
+            else hipLaunchKernelGGL((k_fit_quad<3, false>), g, b, 0, s, c, c0, c1, seq);
+            return;
         default: return;
         }
     }
@@ -2041,6 +2215,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
     const bool fit_quad = !(fq && fq[0] == '0');
+    const char *fu = getenv("FARMS_FIT_UNION");  // A/B aid: 0 = re-gather the winning window
+    const bool fit_ut = !(fu && fu[0] == '0');
     int fit_launches = 0;
     auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
     auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F
@@ -2050,7 +2226,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
                            c1, seq);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * f], s));
         if (fast_fit) {
-            launch_fit(c, h->fr, c0, c1, seq, s, fit_quad);
+            launch_fit(c, h->fr, c0, c1, seq, s, fit_quad, fit_ut);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, c, seq, h->Q + c0, c1 - c0);
         }

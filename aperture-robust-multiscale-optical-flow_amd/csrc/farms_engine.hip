@@ -516,7 +516,11 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
 #pragma unroll
         for (int i = 0; i < len; ++i) {
             const int v = v0 + i;
-            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+            // unconditional load from a clamped index, then select: a load under a
+            // branch is waited for at the branch's end, serializing the column
+            const bool ok = inr && v >= 0 && v < H;
+            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
         }
     };
     auto score_col = [&](int du, const uint4 *col) {
@@ -759,7 +763,11 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
 #pragma unroll
         for (int i = 0; i < len; ++i) {
             const int v = v0 + i;
-            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+            // unconditional load from a clamped index, then select: a load under a
+            // branch is waited for at the branch's end, serializing the column
+            const bool ok = inr && v >= 0 && v < H;
+            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
         }
     };
     // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
@@ -926,13 +934,20 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
 #pragma unroll
         for (int i = 0; i < len; ++i) {
             const int v = v0 + i;
-            col[i] = (inr && v >= 0 && v < H) ? sae_head(c, (uint32_t)(cbase + i)) : make_uint4(0, 0, 0, 0);
+            // unconditional load from a clamped index, then select: a load under a
+            // branch is waited for at the branch's end, serializing the column
+            const bool ok = inr && v >= 0 && v < H;
+            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
         }
     };
     // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
     uint64_t umask = 0;  // visited bits of this lane's union cells: (slot * US + row), slot = column / 4
-#pragma unroll 1
-    for (int du = -2 * FR + j; du <= 2 * FR; du += 4) {
+    constexpr int NC = (US + 3) / 4;  // union columns per lane (the last one absent on some lanes)
+#pragma unroll
+    for (int sl = 0; sl < NC; ++sl) {  // unrolled: the loads of every column are in flight together
+        const int du = -2 * FR + j + 4 * sl;
+        if (du > 2 * FR) continue;
         uint4 col[US];
         load_col(ex + du, ey - 2 * FR, US, col);
         const int u = ex + du;

@@ -1277,20 +1277,6 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
 constexpr int kGroupCells = 256;  // cells per candidate group = one k_chain wavefront (4 bitmap words)
 
 
-// Candidate index (in buffer b) of the first candidate with cell index >= L
-// (cand_lo), and one past the last with cell index <= L (cand_hi); both stay
-// inside L's candidate group.
-__device__ __forceinline__ uint32_t cand_lo(const Ctx &c, int b, int64_t L) {
-    const int64_t w = L >> 6;
-    return c.wo_ring[(int64_t)b * (c.nwords + 1) + w] +
-           (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((1ull << (L & 63)) - 1));
-}
-__device__ __forceinline__ uint32_t cand_hi(const Ctx &c, int b, int64_t L) {
-    const int64_t w = L >> 6;
-    return c.wo_ring[(int64_t)b * (c.nwords + 1) + w] +
-           (uint32_t)__popcll(c.bm_ring[(int64_t)b * c.nwords + w] & ((2ull << (L & 63)) - 1));
-}
-
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling
 // chunks [ch0, ch1)).  A wavefront owns one candidate group (kGroupCells = 256
 // cells = 4 bitmap words, lane = cell of each word); the group's candidates of
@@ -1564,31 +1550,48 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     // second starts at its group's first slot, whose index is the group's
     // first cell index).  Lane l handles rows l and l + 64 (2M+1 <= 127): the
     // lookups of both are in flight before either is used.
+    // All six lookups of both rows are unconditional loads from clamped word
+    // indices (a load under a branch would be waited for at the branch end).
     int a0[2], n0[2], a1[2], n1[2];
+    const uint64_t *bmb = c.bm_ring + (int64_t)buf * c.nwords;
+    const uint32_t *wob = c.wo_ring + (int64_t)buf * (c.nwords + 1);
+    const int wmax = (int)c.nwords - 1;
+    int lo_[2], hi0_[2], hi1_[2], gb_[2];
+    bool has_[2], str_[2];
+    uint64_t bA[2], bB[2], bC[2];
+    uint32_t oA[2], oB[2], oC[2];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
         const int r = lane + 64 * hh;
-        a0[hh] = 0; n0[hh] = 0; a1[hh] = 0; n1[hh] = 0;
-        if (r < nrows) {
-            const int base = (i_lo + r) * H;
-            int l1 = base + j_hi;
-            if (l1 > WHs - 1) l1 = WHs - 1;  // past the end of the sensor: no contribution
-            int l0 = base + j_lo - OFF;
-            l1 -= OFF;
-            if (l0 < 0) l0 = 0;               // outside the stored region: never visited
-            if (l1 > WHl - 1) l1 = WHl - 1;
-            if (l0 <= l1) {
-                const int gb = l1 & ~(kGroupCells - 1);  // first cell of l1's group
-                a0[hh] = (int)cand_lo(c, buf, l0);
-                if (l0 < gb) {
-                    n0[hh] = (int)cand_hi(c, buf, gb - 1) - a0[hh];
-                    a1[hh] = gb;
-                    n1[hh] = (int)cand_hi(c, buf, l1) - gb;
-                } else {
-                    n0[hh] = (int)cand_hi(c, buf, l1) - a0[hh];
-                }
-            }
-        }
+        const int base = (i_lo + (r < nrows ? r : 0)) * H;
+        int l1 = base + j_hi;
+        if (l1 > WHs - 1) l1 = WHs - 1;  // past the end of the sensor: no contribution
+        int l0 = base + j_lo - OFF;
+        l1 -= OFF;
+        if (l0 < 0) l0 = 0;               // outside the stored region: never visited
+        if (l1 > WHl - 1) l1 = WHl - 1;
+        const int gb = l1 & ~(kGroupCells - 1);  // first cell of l1's group
+        has_[hh] = r < nrows && l0 <= l1;
+        str_[hh] = has_[hh] && l0 < gb;          // the range crosses into l1's group
+        lo_[hh] = l0; gb_[hh] = gb;
+        hi0_[hh] = str_[hh] ? gb - 1 : l1;       // end of the first segment
+        hi1_[hh] = l1;
+        const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
+                  wc = min(max(l1 >> 6, 0), wmax);
+        bA[hh] = bmb[wa]; oA[hh] = wob[wa];
+        bB[hh] = bmb[wb]; oB[hh] = wob[wb];
+        bC[hh] = bmb[wc]; oC[hh] = wob[wc];
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        // candidate index of the first candidate >= L (lo) / one past the last <= L (hi)
+        const int lo = (int)(oA[hh] + (uint32_t)__popcll(bA[hh] & ((1ull << (lo_[hh] & 63)) - 1)));
+        const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
+        const int h1 = (int)(oC[hh] + (uint32_t)__popcll(bC[hh] & ((2ull << (hi1_[hh] & 63)) - 1)));
+        a0[hh] = lo;
+        n0[hh] = has_[hh] ? h0 - lo : 0;
+        a1[hh] = gb_[hh];
+        n1[hh] = str_[hh] ? h1 - gb_[hh] : 0;
     }
     int carry = 0, nz = 0;
 #pragma unroll
@@ -1836,14 +1839,20 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     const int w = c0 + work_block() * 4 + wv;
     if (w >= c1) return;
     const int e = c.Q[w];
-    if (!c.valid[e]) return;
-    const int ex = c.x[e];
+    // the event's fields load together with its validity flag
+    const uint32_t vld = c.valid[e];
+    const int ex = c.x[e], ey = c.y[e];
+    const uint32_t teu = c.t[e];
+    // keep the compiler from sinking the field loads below the exits: the four
+    // loads then share one round trip
+    asm volatile("" ::"v"(vld), "v"(ex), "v"(ey), "v"(teu));
+    if (!vld) return;
     if (ex < c.own_lo || ex >= c.own_hi) return;
     const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
     uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap);
     int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
     uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs);
-    pool_event<K>(c, e, ex, c.y[e], c.t[e], buf, lane, s_start, s_row, s_con);
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, s_start, s_row, s_con);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,

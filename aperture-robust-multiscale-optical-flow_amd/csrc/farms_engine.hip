@@ -1729,7 +1729,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         for (int j = 0; j < kShare; ++j) {
             vk0[j] = K;  // empty slot: in no scale
             vL[j] = 0.0;
-            if (b0 + j < b1) {
+            if (j * 64 < nb && b0 + j < b1) {  // (first test wave-uniform)
                 const uint2 en = s_con[b0 + j];
                 vk0[j] = (int)(en.y >> 8);
                 vL[j] = length_of(en);
@@ -1740,8 +1740,10 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) cntk[kk] += (int)__popcll(__ballot(k0 <= kk));
         }
+        const int nj = (nb + 63) >> 6;  // entries per lane at most (wave-uniform)
 #pragma unroll
         for (int j = 0; j < kShare; ++j) {
+            if (j >= nj) break;  // uniform: skip share slots no lane holds
 #pragma unroll
             for (int kk = 0; kk < K; ++kk)
                 if (kk >= vk0[j]) sL[kk] += vL[j];

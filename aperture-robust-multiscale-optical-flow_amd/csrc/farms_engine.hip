@@ -2008,6 +2008,7 @@ struct farms_handle {
     unsigned long long *counters = nullptr;
     bool profiling = false;  // kernel timing events
     bool counting = false;   // work counters (k_stats, per-event candidate counts)
+    bool fit_events = false;  // timing events around every fit launch too
     hipEvent_t ev[8] = {};
     std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
     farms_stats stats{};
@@ -2250,13 +2251,13 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         const uint32_t seq = ++h->seq;
         hipLaunchKernelGGL(k_fit_prep, dim3(ceil_div(std::max(c1 - c0, c0 - p0), 256)), dim3(256), 0, s, c, p0, c0,
                            c1, seq);
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * f], s));
+        if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f], s));
         if (fast_fit) {
             launch_fit(c, h->fr, c0, c1, seq, s, fit_quad, fit_ut);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, c, seq, h->Q + c0, c1 - c0);
         }
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
+        if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
         HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
         if (f == n_fit_chunks - 1) {  // SAE snapshot of the last chunk (streaming state)
@@ -2325,7 +2326,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         // to the end of the last pooling launch
         st.ms_prep = a; st.ms_fit = b; st.ms_pool = d; st.ms_total = (double)a + d;
         double kf = 0, kp = 0;
-        for (int i = 0; i < fit_launches; ++i) {
+        for (int i = 0; i < (h->fit_events ? fit_launches : 0); ++i) {
             float v = 0;
             HIPCHK(hipEventElapsedTime(&v, h->kev[2 * i], h->kev[2 * i + 1]));
             kf += v;
@@ -2469,7 +2470,8 @@ extern "C" int farms_reset(farms_handle *h) {
 extern "C" int farms_set_profiling(farms_handle *h, int enable) {
     if (!h) return fail(FARMS_EINVAL, "null handle");
     h->profiling = enable != 0;
-    h->counting = enable != 0 && enable != FARMS_PROF_TIMING;
+    h->fit_events = enable != 0 && enable != FARMS_PROF_POOL;
+    h->counting = enable != 0 && enable != FARMS_PROF_TIMING && enable != FARMS_PROF_POOL;
     return FARMS_OK;
 }
 

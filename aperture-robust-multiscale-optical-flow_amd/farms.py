@@ -26,6 +26,7 @@ FARMS_ENOMEM = -3
 FARMS_ENODEV = -4
 PROF_TIMING = 1    # farms_set_profiling: HIP events around phases and k_fit / k_pool launches
 PROF_COUNTERS = 2  # ... plus the U_loc / U_pool / candidate / contributor counters
+PROF_POOL = 3      # HIP events around phases and k_pool launches only
 
 # record columns, in the order of src/vFlow.cpp:438
 COLUMNS = ("x", "y", "t", "p", "r_true", "theta_true", "vx", "vy", "r_local", "theta_local", "scale")
@@ -320,7 +321,7 @@ class FlowManager:
 
     def set_profiling(self, on: bool | int) -> None:
         """True: timing events and work counters; PROF_TIMING: timing only."""
-        _check(self._lib, self._lib.farms_set_profiling(self._h, int(on) if not isinstance(on, bool) else (3 if on else 0)))
+        _check(self._lib, self._lib.farms_set_profiling(self._h, int(on) if not isinstance(on, bool) else (255 if on else 0)))
 
     def stats(self) -> dict:
         st = FarmsStats()

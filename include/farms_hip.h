@@ -111,12 +111,15 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
                          farms_records *d_out);
 
 /* Profiling of the next calls: FARMS_PROF_TIMING records HIP events around the
- * phases and every k_fit / k_pool launch (times in farms_stats; negligible
- * cost), FARMS_PROF_COUNTERS also counts U_loc / U_pool / candidates /
- * contributors (an extra kernel pass, ~2% of a call).  0 = off (default); any
- * other nonzero value = both. */
+ * phases and every k_fit / k_pool launch (times in farms_stats; ~1,700 event
+ * records per 50M events, a few % of a call), FARMS_PROF_POOL only around the
+ * phases and the k_pool launches (ms_fit_kernel stays 0), FARMS_PROF_COUNTERS
+ * also counts U_loc / U_pool / candidates / contributors (an extra kernel
+ * pass, ~2% of a call).  0 = off (default); any other value = timing and
+ * counters. */
 #define FARMS_PROF_TIMING 1
 #define FARMS_PROF_COUNTERS 2
+#define FARMS_PROF_POOL 3
 int farms_set_profiling(farms_handle *h, int enable);
 int farms_get_stats(const farms_handle *h, farms_stats *out);
 

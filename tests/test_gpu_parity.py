@@ -152,3 +152,51 @@ def test_out_of_sensor_event_is_rejected():
         ok = fm.process(np.array([1], np.int32), np.array([1], np.int32), np.array([0], np.uint32),
                         np.array([1], np.int32))
         assert ok.n == 1
+
+
+@pytest.mark.parametrize("fs", [3, 5, 7])
+def test_fit_variants_are_bitwise_identical(fs, monkeypatch):
+    """The quad-lane fit (with and without the union tile) and the one-thread
+    fit evaluate the same arithmetic in the same order: bitwise-equal records."""
+    ev = farms.synth_config(3, 150_000)
+    x, y, t, p = ev.relative()
+    outs = []
+    for quad, union in [("1", "1"), ("1", "0"), ("0", "1")]:
+        monkeypatch.setenv("FARMS_FIT_QUAD", quad)
+        monkeypatch.setenv("FARMS_FIT_UNION", union)
+        with farms.FlowManager(720, 1280, fs, 5) as fm:
+            outs.append(fm.process(x, y, t, p))
+    for o in outs[1:]:
+        assert bitwise_equal(outs[0], o)
+
+
+def test_full_size_stream_properties():
+    """BASELINE config 3 at full size (50M events, 1280x720, fs 5): the run is
+    bitwise invariant to chunking, and its first 100k records equal the
+    oracle's run of those 100k events (the path is causal)."""
+    import torch
+
+    ev = farms.synth_config(3)
+    x, y, t, p = ev.relative()
+    n = len(x)
+    assert n == 50_000_000
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(a).to(dev) for a in (x, y, t.view(np.int32), p)]
+    outs = []
+    for fc, pc in [(0, 0), (262_144, 16_384)]:
+        o = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+             for c in farms.COLUMNS[4:]}
+        with farms.FlowManager(720, 1280, 5, 5, fit_chunk=fc, pool_chunk=pc) as fm:
+            fm.process_device(*d, o)
+        outs.append(o)
+    for c in farms.COLUMNS[4:]:
+        a, b = outs[0][c], outs[1][c]
+        if a.dtype == torch.float64:
+            a, b = a.view(torch.int64), b.view(torch.int64)
+        assert torch.equal(a, b), c
+    k = 100_000
+    g = {c: v for c, v in zip(farms.COLUMNS[:4], (x[:k], y[:k], t[:k].astype(np.int32), p[:k]))}
+    g.update({c: outs[0][c][:k].cpu().numpy() for c in farms.COLUMNS[4:]})
+    r = OracleFlow(720, 1280, 5, 5).process(x[:k], y[:k], t[:k], p[:k])
+    assert_parity(g, r)
+    assert int((outs[0]["r_local"] > 0).sum()) > n // 4  # most of the stream is pooled

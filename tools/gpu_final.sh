@@ -20,4 +20,9 @@ rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log
+[ $rc -ne 0 ] && exit $rc
+if [ "${RANKSIM:-0}" = "1" ]; then  # ranks 0, 4, 7 of an N=8 temporal-segment run, one after the other
+  timeout -k 10 900 python3 tools/strip_rank.py --split segments --n 8 --ranks 0,4,7 > gpurun_out/seg8_rank_sim.log 2>&1
+  rc=$?; echo "rank sim rc=$rc"; tail -1 gpurun_out/seg8_rank_sim.log
+fi
 exit $rc

@@ -9,17 +9,19 @@
 //
 // How it runs here:
 //   prep    pixel id per event; stable radix sort of event ids by pixel
-//           (hipCUB) -> per-pixel runs in index order; prev/next links.
-//   sweep 1 (local fit)  events in chunks of C1.  The SAE "as of event e" at
-//           pixel q = the last event at q with index <= e: a dense snapshot of
-//           the SAE at chunk start plus, for pixels touched inside the chunk, a
-//           binary search of that pixel's in-chunk run.  One thread per event.
-//   sweep 2 (pooling)    chunks of C2.  Flow state "as of e" is resolved the
-//           same way against a dense flow snapshot.  A per-chunk bitmap marks
-//           cells that can contribute to any event of the chunk (touched in the
-//           chunk, or carrying valid flow younger than the 500 us kill time at
-//           the chunk's time span); one wavefront per valid event walks the
-//           bitmap rows of its 101 x 101 window, lanes = window rows.
+//           (hipCUB) -> per-pixel runs in index order; prev/next links; a
+//           second sort gives the work order (pooling chunk, 8x8 tile).
+//   sweep 1 (local fit, stream F)  events in chunks of C1.  The SAE "as of
+//           event e" at pixel q = the last event at q with index <= e: a
+//           snapshot of the SAE at chunk start with the pixel's first two
+//           in-chunk events inline (k_fit_prep), a run scan beyond that.
+//           k_fit_quad: four lanes per event, the union of the 9 windows in
+//           an LDS tile, exact integer scores and sums combined over the quad.
+//   sweep 2 (pooling, streams C and P)  chunks of C2 in super-chunks of B.
+//           k_chain keeps every cell's flow state in registers across the B
+//           chunks and writes, per chunk, the candidate list (bitmap + group-
+//           local slots) of cells that can contribute to any of its events;
+//           k_pool pools one valid event per wavefront from that list.
 // Local flow depends only on the SAE, pooling only on local flows and times, so
 // these two sweeps reproduce the sequential semantics exactly.
 //

@@ -1346,10 +1346,20 @@ __global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
     }
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) prefetch(i);
+    // the chunks' stamp spans, lane l holding chunk ch0 + l (read with a
+    // wave-uniform readlane: no memory round trip per chunk)
+    const bool spans_in_regs = ch1 - ch0 <= 64;
+    const uint32_t tmin_l = (spans_in_regs && ch0 + lane < ch1) ? c.ctmin[ch0 + lane] : 0u;
+    const uint32_t tmax_l = (spans_in_regs && ch0 + lane < ch1) ? c.ctmax[ch0 + lane] : 0u;
+    // wait for them here, once: otherwise the loop header waits for every
+    // outstanding load (the prefetches included) before each readlane
+    asm volatile("" ::"v"(tmin_l), "v"(tmax_l));
     for (int ch = ch0; ch < ch1; ++ch) {
         const int b = ch % c.NB;
         const int ce = min((ch + 1) * C2, n);
-        const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
+        const uint32_t tmin = spans_in_regs ? (uint32_t)__builtin_amdgcn_readlane((int)tmin_l, ch - ch0) : c.ctmin[ch];
+        const uint32_t tmax = spans_in_regs ? (uint32_t)__builtin_amdgcn_readlane((int)tmax_l, ch - ch0) : c.ctmax[ch];
+        const int64_t lo = (int64_t)tmin - (int64_t)kKillUs, hi = (int64_t)tmax + (int64_t)kKillUs;
         uint64_t bal[kChainCells];
         uint32_t woff[kChainCells];
         uint32_t acc = (uint32_t)(g * kGroupCells);

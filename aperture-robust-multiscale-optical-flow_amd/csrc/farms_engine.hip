@@ -204,6 +204,14 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
     const int q = G >> 3, r = G & 7, x = b & 7;
     return x * q + (x < r ? x : r) + (b >> 3);
 }
+// Grouped variant: runs of 8 consecutive logical blocks stay on one XCD and
+// the runs go round-robin over the XCDs (locality without uneven shares).
+// Bijective on [0, G) when G is a multiple of 64; other grids keep blockIdx.
+__device__ __forceinline__ int xcd_block_grouped(int b, int G) {
+    if (G & 63) return b;
+    const int x = b & 7, i = b >> 3;  // XCD label, index within the XCD
+    return (i >> 3) * 64 + x * 8 + (i & 7);
+}
 #ifndef FARMS_XCD
 #define FARMS_XCD 1  // 0: plain blockIdx order (A/B aid)
 #endif
@@ -1088,9 +1096,13 @@ template <int FR, bool UT>
 __global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * 64];
-    // (plain block order: an XCD-contiguous split of a 1,024-block fit launch
-    // measured 7% slower, its per-XCD work being uneven)
-    const int w = c0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2);
+    // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
+    // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
+#ifndef FARMS_FIT_XCD
+#define FARMS_FIT_XCD 1
+#endif
+    const int fb = FARMS_FIT_XCD ? xcd_block_grouped((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
     const int e = c.Q[w];

@@ -1,11 +1,14 @@
 // event_io.cpp — see event_io.h.
 #include "event_io.h"
 
+#include <algorithm>
+#include <charconv>
 #include <climits>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <thread>
 
 namespace farms_io {
 namespace {
@@ -50,25 +53,13 @@ void extract(const char *&p, const char *end, T &v, bool &fail) {
 
 }  // namespace
 
-int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventColumns &cols) {
-    // variables declared outside the loop, as vFlow.cpp:147
-    int x = 0, y = 0, pol = 0;
-    unsigned int t = 0;
-    const char *p = text, *end = text + len;
+namespace {
+
+// Lines in [p, end): getline's count (a final line without '\n' counts).
+int64_t count_lines(const char *p, const char *end) {
     int64_t n = 0;
-    while (p < end && (uint64_t)n < max_events) {  // getline && numEvents < NUMEVENTS
+    while (p < end) {
         const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
-        const char *le = nl ? nl : end;
-        const char *q = p;
-        bool fail = false;
-        extract(q, le, x, fail);
-        extract(q, le, y, fail);
-        extract(q, le, t, fail);
-        extract(q, le, pol, fail);
-        cols.X.push_back(x);
-        cols.Y.push_back(y);
-        cols.T.push_back(t);
-        cols.POL.push_back(pol);
         ++n;
         if (!nl) break;
         p = nl + 1;
@@ -76,50 +67,197 @@ int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventCol
     return n;
 }
 
+// Parser state carried from line to line (vFlow.cpp:147 declares the four
+// variables outside the loop). `known` tracks, per field, whether this chunk
+// has assigned it yet; until then its lines carry the value the previous
+// chunk ends with, which the fix-up pass fills in.
+struct Carry {
+    int x = 0, y = 0, pol = 0;
+    unsigned int t = 0;
+};
+
+struct ChunkOut {
+    int64_t first_def[4] = {-1, -1, -1, -1};  // first line (chunk-relative) that assigns field f
+    Carry last;                               // values after the chunk's last line
+};
+
+// Parse `lines` lines of [p, end) into X/Y/T/P.
+void parse_chunk(const char *p, const char *end, int64_t lines, int *X, int *Y, unsigned *T, int *P,
+                 ChunkOut &co) {
+    Carry c;
+    for (int64_t i = 0; i < lines; ++i) {
+        const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+        const char *le = nl ? nl : end;
+        const char *q = p;
+        bool fail = false;
+        // a field is assigned by extract() unless the stream has already failed
+        // or the line ends before it; either way the variable keeps its value
+        bool assigned[4];
+        auto field = [&](int f, auto &v) {
+            const char *w = q;
+            while (w < le && is_space(*w)) ++w;
+            assigned[f] = !fail && w < le;
+            extract(q, le, v, fail);
+        };
+        field(0, c.x);
+        field(1, c.y);
+        field(2, c.t);
+        field(3, c.pol);
+        for (int f = 0; f < 4; ++f)
+            if (assigned[f] && co.first_def[f] < 0) co.first_def[f] = i;
+        X[i] = c.x; Y[i] = c.y; T[i] = c.t; P[i] = c.pol;
+        if (!nl) break;
+        p = nl + 1;
+    }
+    co.last = c;
+}
+
+}  // namespace
+
+int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventColumns &cols, int threads) {
+    const char *end = text + len;
+    // cap the text at max_events lines (getline && numEvents < NUMEVENTS)
+    if (threads <= 0) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        threads = (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+        if (len < ((size_t)1 << 22)) threads = 1;  // small inputs: not worth the threads
+    }
+    // chunk boundaries at line starts
+    std::vector<const char *> cut((size_t)threads + 1);
+    cut[0] = text;
+    for (int k = 1; k < threads; ++k) {
+        const char *q = std::max(cut[(size_t)k - 1], text + len / (size_t)threads * (size_t)k);
+        const char *nl = q < end ? (const char *)memchr(q, '\n', (size_t)(end - q)) : nullptr;
+        cut[(size_t)k] = nl ? nl + 1 : end;
+    }
+    cut[(size_t)threads] = end;
+    std::vector<int64_t> nl((size_t)threads), off((size_t)threads + 1, 0);
+    auto run = [&](auto &&fn) {
+        if (threads == 1) { fn(0); return; }
+        std::vector<std::thread> pool;
+        for (int k = 0; k < threads; ++k) pool.emplace_back(fn, k);
+        for (auto &t : pool) t.join();
+    };
+    run([&](int k) { nl[(size_t)k] = count_lines(cut[(size_t)k], cut[(size_t)k + 1]); });
+    for (int k = 0; k < threads; ++k) off[(size_t)k + 1] = off[(size_t)k] + nl[(size_t)k];
+    const int64_t total = std::min<int64_t>(off[(size_t)threads], (int64_t)std::min<uint64_t>(max_events, INT64_MAX));
+    const size_t base = cols.X.size();
+    cols.X.resize(base + (size_t)total); cols.Y.resize(base + (size_t)total);
+    cols.T.resize(base + (size_t)total); cols.POL.resize(base + (size_t)total);
+    std::vector<ChunkOut> co((size_t)threads);
+    run([&](int k) {
+        const int64_t lo = std::min(off[(size_t)k], total), hi = std::min(off[(size_t)k + 1], total);
+        if (hi > lo)
+            parse_chunk(cut[(size_t)k], cut[(size_t)k + 1], hi - lo, cols.X.data() + base + lo,
+                        cols.Y.data() + base + lo, cols.T.data() + base + lo, cols.POL.data() + base + lo,
+                        co[(size_t)k]);
+    });
+    // fix-up, in chunk order: the leading lines of a chunk that carried a field
+    // before assigning it take the value the previous chunk ended with
+    Carry in;  // the reference's initial values (0)
+    for (int k = 0; k < threads; ++k) {
+        const int64_t lo = std::min(off[(size_t)k], total), hi = std::min(off[(size_t)k + 1], total);
+        if (hi <= lo) continue;
+        const int64_t len_k = hi - lo;
+        const ChunkOut &o = co[(size_t)k];
+        auto upto = [&](int f) { return o.first_def[f] < 0 ? len_k : o.first_def[f]; };
+        for (int64_t i = 0; i < upto(0); ++i) cols.X[base + (size_t)(lo + i)] = in.x;
+        for (int64_t i = 0; i < upto(1); ++i) cols.Y[base + (size_t)(lo + i)] = in.y;
+        for (int64_t i = 0; i < upto(2); ++i) cols.T[base + (size_t)(lo + i)] = in.t;
+        for (int64_t i = 0; i < upto(3); ++i) cols.POL[base + (size_t)(lo + i)] = in.pol;
+        if (o.first_def[0] >= 0) in.x = o.last.x;
+        if (o.first_def[1] >= 0) in.y = o.last.y;
+        if (o.first_def[2] >= 0) in.t = o.last.t;
+        if (o.first_def[3] >= 0) in.pol = o.last.pol;
+    }
+    return total;
+}
+
 bool read_events(const std::string &path, uint64_t max_events, EventColumns &cols, int64_t &n_read) {
     n_read = 0;
-    std::ifstream f(path.c_str(), std::ios::binary);
-    if (!f.is_open()) return false;
-    std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::string text;
+    char buf[1 << 16];
+    if (fseek(f, 0, SEEK_END) == 0) {
+        const long sz = ftell(f);
+        if (sz > 0) text.reserve((size_t)sz);
+        fseek(f, 0, SEEK_SET);
+    }
+    size_t got;
+    while ((got = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, got);
+    fclose(f);
     n_read = parse_events(text.data(), text.size(), max_events, cols);
     return true;
 }
 
 static size_t put_record(char *dst, const farms_records &r, int64_t i) {
-    return (size_t)snprintf(dst, 256, "%d %d %d %d %g %g %g %g %g %g %d\n", r.x[i], r.y[i], r.t[i], r.p[i],
-                            r.r_true[i], r.theta_true[i], r.vx[i], r.vy[i], r.r_local[i], r.theta_local[i],
-                            r.scale[i]);
+    char *p = dst, *const end = dst + 256;
+    const int32_t iv[4] = {r.x[i], r.y[i], r.t[i], r.p[i]};
+    for (int k = 0; k < 4; ++k) {
+        p = std::to_chars(p, end, iv[k]).ptr;
+        *p++ = ' ';
+    }
+    const double dv[6] = {r.r_true[i], r.theta_true[i], r.vx[i], r.vy[i], r.r_local[i], r.theta_local[i]};
+    for (int k = 0; k < 6; ++k) {
+        p = std::to_chars(p, end, dv[k], std::chars_format::general, 6).ptr;
+        *p++ = ' ';
+    }
+    p = std::to_chars(p, end, r.scale[i]).ptr;
+    *p++ = '\n';
+    return (size_t)(p - dst);
 }
 
 std::string format_records(const farms_records &r, int64_t begin, int64_t end) {
     std::string out;
+    out.reserve((size_t)(end - begin) * 72);
     char line[256];
     for (int64_t i = begin; i < end; ++i) out.append(line, put_record(line, r, i));
     return out;
 }
 
+// Blocks of kBlock records are formatted by up to 16 threads at once, each
+// into its own buffer, and written in order: the file is byte-identical to a
+// sequential write, and host memory stays bounded (~16 x 8 MB).
 bool write_records(const std::string &path, const farms_records &r, int64_t n) {
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return false;
-    std::vector<char> buf(1 << 22);
-    size_t used = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        if (buf.size() - used < 256) { fwrite(buf.data(), 1, used, f); used = 0; }
-        used += put_record(buf.data() + used, r, i);
+    constexpr int64_t kBlock = 1 << 17;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nt = (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+    std::vector<std::string> bufs((size_t)nt);
+    bool ok = true;
+    for (int64_t b0 = 0; b0 < n && ok; b0 += kBlock * nt) {
+        std::vector<std::thread> pool;
+        int used = 0;
+        for (int k = 0; k < nt; ++k) {
+            const int64_t lo = b0 + k * kBlock, hi = std::min(n, lo + kBlock);
+            if (lo >= hi) break;
+            ++used;
+            if (nt == 1) bufs[0] = format_records(r, lo, hi);
+            else pool.emplace_back([&bufs, &r, k, lo, hi] { bufs[(size_t)k] = format_records(r, lo, hi); });
+        }
+        for (auto &t : pool) t.join();
+        for (int k = 0; k < used; ++k)
+            ok = ok && fwrite(bufs[(size_t)k].data(), 1, bufs[(size_t)k].size(), f) == bufs[(size_t)k].size();
     }
-    fwrite(buf.data(), 1, used, f);
-    return fclose(f) == 0;
+    return fclose(f) == 0 && ok;
 }
 
 }  // namespace farms_io
 
-extern "C" int64_t farms_io_parse(const char *text, int64_t len, int64_t max_events, int32_t *x, int32_t *y,
-                                  uint32_t *t, int32_t *p, int64_t cap) {
+extern "C" int64_t farms_io_parse_threads(const char *text, int64_t len, int64_t max_events, int32_t *x,
+                                          int32_t *y, uint32_t *t, int32_t *p, int64_t cap, int threads) {
     farms_io::EventColumns cols;
-    const int64_t n = farms_io::parse_events(text, (size_t)len, (uint64_t)max_events, cols);
+    const int64_t n = farms_io::parse_events(text, (size_t)len, (uint64_t)max_events, cols, threads);
     if (n > cap) return -1;
     for (int64_t i = 0; i < n; ++i) { x[i] = cols.X[i]; y[i] = cols.Y[i]; t[i] = cols.T[i]; p[i] = cols.POL[i]; }
     return n;
+}
+
+extern "C" int64_t farms_io_parse(const char *text, int64_t len, int64_t max_events, int32_t *x, int32_t *y,
+                                  uint32_t *t, int32_t *p, int64_t cap) {
+    return farms_io_parse_threads(text, len, max_events, x, y, t, p, cap, 0);
 }
 
 extern "C" int64_t farms_io_format(const farms_records *r, int64_t n, char *out, int64_t cap) {
@@ -128,4 +266,8 @@ extern "C" int64_t farms_io_format(const farms_records *r, int64_t n, char *out,
     memcpy(out, s.data(), s.size());
     out[s.size()] = '\0';
     return (int64_t)s.size();
+}
+
+extern "C" int farms_io_write(const char *path, const farms_records *r, int64_t n) {
+    return farms_io::write_records(path, *r, n) ? 0 : -1;
 }

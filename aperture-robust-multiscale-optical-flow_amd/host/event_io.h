@@ -26,8 +26,11 @@ struct EventColumns {
 };
 
 // Parse the events of `text` (a whole file) into cols, at most max_events
-// lines.  Returns the number of events appended.
-int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventColumns &cols);
+// lines.  Returns the number of events appended.  Chunks of lines are parsed
+// on `threads` threads (0: up to 16, one for inputs under 4 MB); the values a
+// chunk's leading lines carry over from the previous line are filled in
+// afterwards, so the result equals the one-thread parse.
+int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventColumns &cols, int threads = 0);
 
 // Read and parse a file.  Returns false if it cannot be opened.
 bool read_events(const std::string &path, uint64_t max_events, EventColumns &cols, int64_t &n_read);

@@ -23,6 +23,10 @@ def io():
         ctypes.c_int64]
     lib.farms_io_format.restype = ctypes.c_int64
     lib.farms_io_format.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+    lib.farms_io_parse_threads.restype = ctypes.c_int64
+    lib.farms_io_parse_threads.argtypes = lib.farms_io_parse.argtypes + [ctypes.c_int]
+    lib.farms_io_write.restype = ctypes.c_int
+    lib.farms_io_write.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64]
     return lib
 
 
@@ -94,3 +98,100 @@ def test_record_format_matches_ostream_defaults(io):
     assert lines[3] == "4 8 2147483647 0 1e-07 -2.5 0.1 100000 5 1 25"
     # the Python formatter produces the same text
     assert rec.to_text().splitlines() == lines
+
+
+def _libc_g(v: float) -> str:
+    """glibc printf("%g") of one double: what `ostream << double` prints."""
+    libc = ctypes.CDLL(None)
+    b = ctypes.create_string_buffer(64)
+    libc.snprintf(b, 64, b"%g", ctypes.c_double(v))
+    return b.value.decode()
+
+
+def test_float_format_matches_printf_g(io):
+    """The writer's to_chars path equals printf %g on rounding boundaries,
+    exponent switch points, subnormals, signed zero and non-finite values."""
+    rng = np.random.default_rng(7)
+    vals = [0.0, -0.0, float("inf"), -float("inf"), float("nan"), -float("nan"), 5e-324, 2.2250738585072014e-308,
+            1.7976931348623157e308, 9.999995, 9.9999949999, 0.00010000005, 0.0001, 9.99999e-05, 123456.5,
+            999999.5, 999999.4, 1e6, 1e-5, 0.5, 2.5, 1234565.0]
+    vals += list(rng.standard_normal(400) * 10.0 ** rng.integers(-12, 12, 400))
+    vals += list(np.round(rng.standard_normal(200), 6))  # many exact ties of the 6-digit rounding
+    n = len(vals)
+    rec = farms.Records(n)
+    rec.x[:] = rng.integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    for col in ("r_true", "theta_true", "vx", "vy", "r_local", "theta_local"):
+        getattr(rec, col)[:] = vals
+        vals = vals[1:] + vals[:1]
+    c = rec.as_c()
+    buf = ctypes.create_string_buffer(n * 160)
+    assert io.farms_io_format(ctypes.byref(c), n, buf, n * 160) > 0
+    for i, line in enumerate(buf.value.decode().splitlines()):
+        f = line.split(" ")
+        assert f[0] == str(int(rec.x[i]))
+        want = [_libc_g(float(getattr(rec, col)[i])) for col in ("r_true", "theta_true", "vx", "vy", "r_local",
+                                                                     "theta_local")]
+        assert f[4:10] == want, (i, f[4:10], want)
+
+
+def test_threaded_writer_equals_formatter(io, tmp_path):
+    """write_records formats blocks of 128k records on several threads; the file
+    equals the one-pass formatter's text byte for byte."""
+    n = 700_000
+    rng = np.random.default_rng(3)
+    rec = farms.Records(n)
+    rec.x[:] = np.arange(n, dtype=np.int32)
+    rec.y[:] = rng.integers(0, 720, n)
+    rec.t[:] = np.arange(n, dtype=np.int32) * 3
+    rec.p[:] = rng.integers(0, 2, n)
+    for col in ("r_true", "theta_true", "vx", "vy", "r_local", "theta_local"):
+        getattr(rec, col)[:] = rng.standard_normal(n) * 100
+    rec.scale[:] = rng.integers(0, 11, n) * 5
+    c = rec.as_c()
+    path = tmp_path / "out.txt"
+    assert io.farms_io_write(str(path).encode(), ctypes.byref(c), n) == 0
+    cap = n * 160
+    buf = ctypes.create_string_buffer(cap)
+    m = io.farms_io_format(ctypes.byref(c), n, buf, cap)
+    assert path.read_bytes() == buf.raw[:m]
+
+
+def _parse_arrays(io, text: bytes, threads: int, max_events=1 << 40):
+    cap = text.count(b"\n") + 2
+    x, y, p = (np.zeros(cap, np.int32) for _ in range(3))
+    t = np.zeros(cap, np.uint32)
+    n = io.farms_io_parse_threads(text, len(text), max_events, x.ctypes.data, y.ctypes.data, t.ctypes.data,
+                                  p.ctypes.data, cap, threads)
+    assert n >= 0
+    return n, x[:n], y[:n], t[:n], p[:n]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_chunk_parallel_parse_equals_one_thread(io, seed):
+    """Lines are parsed in chunks on several threads; fields a chunk's leading
+    lines carry over from earlier lines (short, blank, failed lines) are filled
+    in afterwards. Any thread count gives the one-thread result, including
+    chunks made only of carrying lines and a max_events cap inside a chunk."""
+    rng = np.random.default_rng(seed)
+    kinds = [b"%d %d %d %d", b"%d %d", b"%d", b"", b"   ", b"%d %d x 1", b"%d -%d %d -1", b"99999999999 %d %d %d",
+             b"%d %d %d %d\r", b"a b c d", b"%d\t%d  %d %d extra"]
+    lines = []
+    for i in range(3000):
+        k = kinds[rng.integers(0, len(kinds))] if rng.random() < 0.5 else kinds[0]
+        vals = tuple(int(v) for v in rng.integers(0, 5000, k.count(b"%d")))
+        lines.append(k % vals if vals else k)
+    if seed == 1:  # a long run of carrying lines, longer than a chunk
+        lines[1000:2500] = [b""] * 1500
+    text = b"\n".join(lines) + (b"" if seed == 2 else b"\n")
+    ref = _parse_arrays(io, text, 1)
+    for threads in (2, 3, 7, 16):
+        got = _parse_arrays(io, text, threads)
+        assert got[0] == ref[0]
+        for a, b in zip(got[1:], ref[1:]):
+            assert np.array_equal(a, b), threads
+    for cap in (1, 777, 2999):
+        r1 = _parse_arrays(io, text, 1, cap)
+        r7 = _parse_arrays(io, text, 7, cap)
+        assert r1[0] == r7[0] == cap
+        for a, b in zip(r1[1:], r7[1:]):
+            assert np.array_equal(a, b)

@@ -132,10 +132,16 @@ int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventCol
     }
     cut[(size_t)threads] = end;
     std::vector<int64_t> nl((size_t)threads), off((size_t)threads + 1, 0);
-    auto run = [&](auto &&fn) {
-        if (threads == 1) { fn(0); return; }
+    auto run = [&](auto &&fn) {  // fn(k) for every chunk k; inline for chunks no thread could take
         std::vector<std::thread> pool;
-        for (int k = 0; k < threads; ++k) pool.emplace_back(fn, k);
+        int k = 0;
+        if (threads > 1) {
+            try {
+                for (; k < threads; ++k) pool.emplace_back(fn, k);
+            } catch (...) {
+            }
+        }
+        for (int j = k; j < threads; ++j) fn(j);
         for (auto &t : pool) t.join();
     };
     run([&](int k) { nl[(size_t)k] = count_lines(cut[(size_t)k], cut[(size_t)k + 1]); });
@@ -234,8 +240,16 @@ bool write_records(const std::string &path, const farms_records &r, int64_t n) {
             const int64_t lo = b0 + k * kBlock, hi = std::min(n, lo + kBlock);
             if (lo >= hi) break;
             ++used;
-            if (nt == 1) bufs[0] = format_records(r, lo, hi);
-            else pool.emplace_back([&bufs, &r, k, lo, hi] { bufs[(size_t)k] = format_records(r, lo, hi); });
+            auto job = [&bufs, &r, k, lo, hi] { bufs[(size_t)k] = format_records(r, lo, hi); };
+            bool spawned = false;
+            if (nt > 1) {
+                try {
+                    pool.emplace_back(job);
+                    spawned = true;
+                } catch (...) {  // no thread available: format this block here
+                }
+            }
+            if (!spawned) job();
         }
         for (auto &t : pool) t.join();
         for (int k = 0; k < used; ++k)

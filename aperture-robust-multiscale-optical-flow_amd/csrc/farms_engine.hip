@@ -2425,6 +2425,16 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->own_hi = prm->own_x1 > 0 ? prm->own_x1 : prm->width;
     h->WH = (int64_t)h->WR * prm->height;
     h->J = prm->window_jump; h->M = prm->max_window; h->K = K;
+    if (h->fr == 3) {  // fs 7 (169-cell fits, fewer valid events): measured best at C4, -10% per step
+        h->fit_chunk = 2 * kDefaultFitChunk;
+        h->pool_chunk = 2 * kDefaultPoolChunk;
+        h->pool_batch = kDefaultPoolBatch / 2;
+    }
+    {  // smaller sensors pool fewer events per chunk: the default scales with the
+       // sensor's linear size (nearest power of two; 320x320: 2048, measured best)
+        const double target = h->pool_chunk * std::sqrt((double)h->W * h->H / (1280.0 * 720.0));
+        while (h->pool_chunk > 1024 && h->pool_chunk > target * std::sqrt(2.0)) h->pool_chunk /= 2;
+    }
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
     if (prm->pool_batch > 0) h->pool_batch = prm->pool_batch;

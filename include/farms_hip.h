@@ -44,8 +44,8 @@ typedef struct {
     int32_t window_jump;  /* pooling scale step, reference 5 */
     int32_t max_window;   /* largest pooling radius, reference 50 */
     int32_t device;       /* HIP device ordinal */
-    int32_t fit_chunk;    /* events per local-fit chunk, 0 = default */
-    int32_t pool_chunk;   /* events per pooling chunk, 0 = default */
+    int32_t fit_chunk;    /* events per local-fit chunk, 0 = default (65536; 131072 at filtersize 7) */
+    int32_t pool_chunk;   /* events per pooling chunk, 0 = default (8192, 16384 at filtersize 7; less on sensors under 1280x720) */
     /* spatial strips (multi-GPU): the handle stores columns [region_x0,
      * region_x0 + region_width) of the width x height sensor and pools only the
      * events of columns [own_x0, own_x1); events of the other stored columns are
@@ -56,7 +56,7 @@ typedef struct {
      * sensor), owned records are bitwise those of a whole-sensor run. */
     int32_t region_x0, region_width;
     int32_t own_x0, own_x1;
-    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64) */
+    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64; 32 at filtersize 7) */
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA

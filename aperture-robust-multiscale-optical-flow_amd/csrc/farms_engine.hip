@@ -207,10 +207,14 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
 // Grouped variant: runs of 8 consecutive logical blocks stay on one XCD and
 // the runs go round-robin over the XCDs (locality without uneven shares).
 // Bijective on [0, G) when G is a multiple of 64; other grids keep blockIdx.
+#ifndef FARMS_FIT_RUN
+#define FARMS_FIT_RUN 8  // consecutive blocks per XCD run
+#endif
 __device__ __forceinline__ int xcd_block_grouped(int b, int G) {
-    if (G & 63) return b;
+    constexpr int R = FARMS_FIT_RUN;
+    if (G % (8 * R)) return b;
     const int x = b & 7, i = b >> 3;  // XCD label, index within the XCD
-    return (i >> 3) * 64 + x * 8 + (i & 7);
+    return (i / R) * (8 * R) + x * R + (i % R);
 }
 #ifndef FARMS_XCD
 #define FARMS_XCD 1  // 0: plain blockIdx order (A/B aid)

@@ -69,8 +69,16 @@ def cpu_baseline(sample, width, height, fs, jump, maxw):
     t0 = time.perf_counter()
     ref = of.process(x, y, t, p)
     dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu)
+    except OSError:
+        pass
     return ref, {"value": len(sample) / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
-            "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, {dt:.1f} s"}
+                 "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, "
+                           f"{dt:.1f} s",
+                 "cpu_model": cpu, "host_threads": os.cpu_count()}
 
 
 def parity_vs_cpu(ref, out, k):

@@ -113,6 +113,7 @@ struct CandVal {
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
+constexpr int kPoolValWords = 3 * 64 + 8;  // k_pool phase B: {L, L cos, L sin} and k0 of 64 entries, 8-B words
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -1472,37 +1473,6 @@ __device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, i
     return lo;
 }
 
-// Transposed butterfly over P = 2^LP slots per lane: at step S each lane keeps
-// the slots whose bit S equals its lane bit S and adds the partner's copy, so
-// step S moves P / 2^(S+1) values; after LP steps the lane holds one slot, and
-// the remaining steps are a plain butterfly.  On return v[0] is the wave total
-// of slot (lane & (P - 1)).  Every slot is combined by the same tree (a + b is
-// commutative), so slots with bitwise-equal lane partials get bitwise-equal
-// totals.
-template <int S, int LP, int N>
-__device__ __forceinline__ void tsum_step(double (&v)[N], int lane) {
-    if constexpr (S < 6) {
-        if constexpr (S < LP) {
-            constexpr int half = N >> (S + 1);
-            const bool hi = (lane >> S) & 1;
-#pragma unroll
-            for (int p = 0; p < half; ++p) {
-                const double lo = v[2 * p], up = v[2 * p + 1];
-                const double send = hi ? lo : up, keep = hi ? up : lo;
-                v[p] = keep + xch<S>(send);
-            }
-        } else {
-            v[0] = v[0] + xch<S>(v[0]);
-        }
-        tsum_step<S + 1, LP, N>(v, lane);
-    }
-}
-template <int LP, int N>
-__device__ __forceinline__ void tsum(double (&v)[N], int lane) {
-    static_assert(N == (1 << LP), "slot count");
-    tsum_step<0, LP, N>(v, lane);
-}
-
 // Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
 // 16-lane row, then the row broadcasts of lanes 15 and 31.
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -1543,19 +1513,23 @@ __device__ __forceinline__ double wave_max(double v) {
 //   Phase A: lanes scan the flattened candidates 64 at a time (coalesced 16-B
 //   headers), resolve each cell's state as of e, and compact the contributors
 //   (valid flow, |dt| < 500 us) into LDS in ascending cell order (ballot).
-//   Phase B: lane l accumulates a contiguous share of the contributor list into
-//   every scale that contains the cell, then a fixed butterfly sums the lanes.
+//   Phase B: lane g*K + k sums quantity g (L, L cos, L sin) of scale k over the
+//   staged list sequentially, in the reference's raster order (vFlow.cpp:998-
+//   1021): the per-scale sums, means and the first strict maximum are bitwise
+//   those of the reference given the same local flows.
 // The summation order depends only on the contributor list, so results are
-// bitwise independent of chunking and streaming splits, and identical
-// contributor sets give identical scale sums (tie rule of vFlow.cpp:1161).
+// bitwise independent of chunking and streaming splits.
 // Pooling of one valid owned event e at (ex, ey, teu) by the calling wave,
 // against candidate buffer buf.  LDS (private to the wave): s_start bit f set
 // iff a non-empty row segment starts at flattened candidate position f;
 // s_row the non-empty segments in order {row, candidate index - flattened
-// index}; s_con the staged contributors {ref, kind | k0 << 8}.
+// index}; s_con the staged contributors {ref, kind | k0 << 8}; s_val / s_k0
+// the values {L, L cos, L sin} and k0 of 64 staged entries.
 template <int K>
 __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                           uint64_t *s_start, int2 *s_row, uint2 *s_con) {
+                                           uint64_t *s_start, int2 *s_row, uint2 *s_con, double *s_val,
+                                           uint8_t *s_k0) {
+    static_assert(3 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
     const int W = c.W, H = c.H, M = c.M, J = c.J;
@@ -1715,33 +1689,32 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         __builtin_amdgcn_wave_barrier();
         return ncon;
     };
-    auto length_of = [&](uint2 en) -> double {
+    // Address of a staged contributor's {L, L cos, L sin}: the candidate's
+    // snapshot (kind 0) or first in-chunk flow (kind 1), or an event's flow
+    // (kind 2); every form is three consecutive doubles.
+    auto value_ptr = [&](uint2 en) -> const double * {
         const uint32_t kind = en.y & 0xFF;
-        if (kind == 0) return cval[en.x].L_snap;
-        if (kind == 1) return cval[en.x].L1;
-        return c.evf[en.x].L;
+        const double *pc = reinterpret_cast<const double *>(cval + en.x) + 3 * (kind & 1);
+        const double *pe = reinterpret_cast<const double *>(c.evf + en.x);
+        return kind == 2 ? pe : pc;
     };
-    auto vec_of = [&](uint2 en, double &Lc, double &Ls) {
-        const uint32_t kind = en.y & 0xFF;
-        if (kind == 0) { Lc = cval[en.x].Lc_snap; Ls = cval[en.x].Ls_snap; }
-        else if (kind == 1) { Lc = cval[en.x].Lc1; Ls = cval[en.x].Ls1; }
-        else { Lc = c.evf[en.x].Lc; Ls = c.evf[en.x].Ls; }
-    };
-    auto value_of = [&](uint2 en, double &L, double &Lc, double &Ls) {
-        const uint32_t kind = en.y & 0xFF;
-        if (kind == 0) { const CandVal &v = cval[en.x]; L = v.L_snap; Lc = v.Lc_snap; Ls = v.Ls_snap; }
-        else if (kind == 1) { const CandVal &v = cval[en.x]; L = v.L1; Lc = v.Lc1; Ls = v.Ls1; }
-        else { const FlowCell fe = c.evf[en.x]; L = fe.L; Lc = fe.Lc; Ls = fe.Ls; }
-    };
-    // ---- phase B1: length sum per scale, lane l taking a contiguous share of
-    // each staged batch; contributor count per scale from ballots (scalar)
-    constexpr int kShare = kPoolCap / 64;
-    double sL[K];
-    int cntk[K];           // wave-uniform
-    double vL[kShare];     // the lane's staged lengths (last pass)
-    int vk0[kShare];
+    // ---- phase B: the per-scale sums in the reference's order.  vFlow.cpp:998-
+    // 1021 accumulates each scale from 0, cell by cell, i ascending then j
+    // ascending.  The staged list holds the contributors of the largest window in
+    // exactly that order (row slices in row order, ascending cells within a row;
+    // a cell the W-1 clip aliases into two rows appears twice, as the reference
+    // visits it twice), and scale k visits the subsequence of entries with
+    // k0 <= k.  Lane g*K + k (g = 0: L, 1: L cos(theta), 2: L sin(theta)) adds
+    // entry after entry and skips non-members: the reference's additions in the
+    // reference's order.  Values reach LDS 64 entries at a time; the loads of
+    // the next 64 are in flight while the current ones are summed.  Counts per
+    // scale are integers (ballots, any order).
+    const int grp = lane / K < 2 ? lane / K : 2;  // lanes past 3K: a spare copy of group 2
+    const int kk = lane - grp * K;
+    double acc = 0.0;
+    int cntk[K];  // wave-uniform
 #pragma unroll
-    for (int k = 0; k < K; ++k) { sL[k] = 0.0; cntk[k] = 0; }
+    for (int k = 0; k < K; ++k) cntk[k] = 0;
     int npass = 1, ncon_total = 0;
     for (int pass = 0; pass < npass; ++pass) {
         if (pass) {
@@ -1751,95 +1724,61 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         ncon_total = collect(pass);
         npass = ncon_total > kPoolCap ? (ncon_total + kPoolCap - 1) / kPoolCap : 1;
         const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
-        // this lane's share (<= kShare entries): all value loads in flight together
-        const int b0 = nb * lane / 64, b1 = nb * (lane + 1) / 64;
+        // entry b0 + lane of the sub-batch at b0: its values and k0 (K: in no scale)
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+        int wk = K;
+        auto fetch = [&](int b0) {
+            const int b = b0 + lane;
+            const uint2 en = b < nb ? s_con[b] : make_uint2((uint32_t)e, 2u | ((uint32_t)K << 8));
+            const double *pv = value_ptr(en);
+            w0 = pv[0]; w1 = pv[1]; w2 = pv[2];
+            wk = (int)(en.y >> 8);
+        };
+        if (nb > 0) fetch(0);
+        for (int b0 = 0; b0 < nb; b0 += 64) {
 #pragma unroll
-        for (int j = 0; j < kShare; ++j) {
-            vk0[j] = K;  // empty slot: in no scale
-            vL[j] = 0.0;
-            if (j * 64 < nb && b0 + j < b1) {  // (first test wave-uniform)
-                const uint2 en = s_con[b0 + j];
-                vk0[j] = (int)(en.y >> 8);
-                vL[j] = length_of(en);
-            }
-        }
-        for (int r0 = 0; r0 < nb; r0 += 64) {  // counts: contributor r0 + lane
-            const int k0 = r0 + lane < nb ? (int)(s_con[r0 + lane].y >> 8) : K;
+            for (int k = 0; k < K; ++k) cntk[k] += (int)__popcll(__ballot(wk <= k));
+            // the previous sub-batch's reads are done (wave-private LDS)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            s_val[3 * lane] = w0; s_val[3 * lane + 1] = w1; s_val[3 * lane + 2] = w2;
+            s_k0[lane] = (uint8_t)wk;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (b0 + 64 < nb) fetch(b0 + 64);
+            const int cnt = min(64, nb - b0);
+            const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+#pragma unroll 1
+            for (int r = 0; r < cnt; r += 4) {  // entries past cnt have k0 = K: no scale adds them
+                const uint32_t k4 = k4p[r >> 2];
 #pragma unroll
-            for (int kk = 0; kk < K; ++kk) cntk[kk] += (int)__popcll(__ballot(k0 <= kk));
-        }
-        const int nj = (nb + 63) >> 6;  // entries per lane at most (wave-uniform)
-#pragma unroll
-        for (int j = 0; j < kShare; ++j) {
-            if (j >= nj) break;  // uniform: skip share slots no lane holds
-#pragma unroll
-            for (int kk = 0; kk < K; ++kk)
-                if (kk >= vk0[j]) sL[kk] += vL[j];
-        }
-    }
-    // wave totals: lane l holds the length sum of scale l mod 2^LP
-    constexpr int LP = K <= 2 ? 1 : (K <= 4 ? 2 : (K <= 8 ? 3 : 4));
-    double slot[1 << LP];
-#pragma unroll
-    for (int q = 0; q < (1 << LP); ++q) slot[q] = q < K ? sL[q] : 0.0;
-    tsum<LP>(slot, lane);
-    // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
-    // the winner is the lowest k whose mean equals the maximum, if it is > 0
-    const int sl = lane & ((1 << LP) - 1);
-    int cnt_sl = 0;
-#pragma unroll
-    for (int kk = 0; kk < K; ++kk) cnt_sl = sl == kk ? cntk[kk] : cnt_sl;
-    const bool is_len = sl < K;
-    const double mean = is_len && cnt_sl > 0 ? slot[0] / (double)cnt_sl : 0.0;
-    const double maxv = wave_max(mean);
-    int mi = 0, cnt_mi = 0;
-    if (maxv > 0) {
-        const uint64_t hit = __ballot(is_len && mean == maxv);
-        const int lw = __builtin_ctzll(hit);
-        mi = lw & ((1 << LP) - 1);
-#pragma unroll
-        for (int kk = 0; kk < K; ++kk) cnt_mi = mi == kk ? cntk[kk] : cnt_mi;
-    }
-    // ---- phase B2: mean vector of the winning scale (vFlow.cpp:1067-1075)
-    double sXY[2] = {0.0, 0.0};
-    if (maxv > 0 && npass == 1) {  // the batch is still staged; the lane's scales are in registers
-        const int b0 = ncon_total * lane / 64;
-        double vC[kShare], vS[kShare];
-#pragma unroll
-        for (int j = 0; j < kShare; ++j) {
-            vC[j] = 0.0; vS[j] = 0.0;
-            if (vk0[j] <= mi) vec_of(s_con[b0 + j], vC[j], vS[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < kShare; ++j)
-            if (vk0[j] <= mi) { sXY[0] += vC[j]; sXY[1] += vS[j]; }
-    } else if (maxv > 0) {
-        for (int pass = 0; pass < npass; ++pass) {
-            if (npass > 1) {  // re-stage batch `pass` (a single batch is still in LDS)
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                collect(pass);
-            }
-            const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
-            for (int b = nb * lane / 64; b < nb * (lane + 1) / 64; ++b) {
-                const uint2 en = s_con[b];
-                if ((int)(en.y >> 8) <= mi) {
-                    double L, Lc, Ls;
-                    value_of(en, L, Lc, Ls);
-                    sXY[0] += Lc;
-                    sXY[1] += Ls;
+                for (int u = 0; u < 4; ++u) {
+                    const int k0 = (int)((k4 >> (8 * u)) & 0xFFu);
+                    const double v = s_val[3 * (r + u) + grp];
+                    acc = kk >= k0 ? acc + v : acc;
                 }
             }
         }
     }
-    tsum<1>(sXY, lane);  // even lanes: sum of Lc, odd lanes: sum of Ls
-    const double sX = sXY[0], sY = xch<0>(sXY[0]);
+    // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
+    // the winner is the lowest k whose mean equals the maximum, if it is > 0
+    int cnt_kk = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt_kk = kk == k ? cntk[k] : cnt_kk;
+    const bool is_len = lane < K;
+    const double mean = is_len && cnt_kk > 0 ? acc / (double)cnt_kk : 0.0;
+    const double maxv = wave_max(mean);
+    const int mi = maxv > 0 ? __builtin_ctzll(__ballot(is_len && mean == maxv)) : 0;
+    const double sx = __shfl(acc, K + mi, 64), sy = __shfl(acc, 2 * K + mi, 64);
     if (lane == 0) {
         double gx, gy;
         int sc;
         if (maxv > 0) {
-            gx = sX / (double)cnt_mi;
-            gy = sY / (double)cnt_mi;
+            int cnt_mi = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) cnt_mi = mi == k ? cntk[k] : cnt_mi;
+            gx = sx / (double)cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
+            gy = sy / (double)cnt_mi;
             sc = mi * J;
         } else {  // vFlow.cpp:1085-1094
             const FlowCell self = c.evf[e];
@@ -1862,7 +1801,7 @@ template <int K>
 __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
     // LDS per wave, sized for maxWindow M at launch (pool_lds_bytes): segment-
     // start bitmap over the flattened window, <= 2 row segments per window
-    // row, kPoolCap staged contributors
+    // row, kPoolCap staged contributors, the values and k0 of 64 of them
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1879,10 +1818,12 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     if (!vld) return;
     if (ex < c.own_lo || ex >= c.own_hi) return;
     const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap);
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap + kPoolValWords);
     int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
     uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs);
-    pool_event<K>(c, e, ex, ey, teu, buf, lane, s_start, s_row, s_con);
+    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + kPoolCap);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, s_start, s_row, s_con, s_val, s_k0);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -2119,7 +2060,7 @@ int reset_surfaces(farms_handle *h) {
 template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap);
+    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap + kPoolValWords);
     hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), lds, s, c, c0, c1);
 }
 

@@ -126,6 +126,14 @@ def load_hip_library() -> ctypes.CDLL:
     global _hip
     if _hip is not None:
         return _hip
+    # torch wheels ship their own HIP runtime under the same SONAME
+    # (libamdhip64.so.7).  Whichever copy is loaded first serves the whole
+    # process, and torch's GPU init fails on the system copy, so in a process
+    # that has torch, let torch load its runtime before this library binds.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     # FARMS_HIP_LIB: an alternative build of the same library (tuning A/B runs
     # of tools/, e.g. `make -C ... variant NAME=x DEFS=...`); never set by the
     # tests, the bench or the driver entry points

@@ -29,6 +29,7 @@
 
 struct farms_oracle {
     int W, H;
+    int serial; /* vFlowManager::run semantics (farms_oracle.h) */
     int frad, plane_size, min_inliers;
     int window_jump, max_window, nscales;
     /* cSurf (vFlow.h:51): stored Event x, y, stamp per cell, x-major (EventMatrix.h:32-33) */
@@ -329,8 +330,8 @@ int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
         const unsigned int tu = t_rel[e];
         const double et = (double)tu;
         const size_t c = (size_t)ex * H + ey;
-        o->last_time[c] = et; /* vFlow.cpp:264 */
-        o->cs_x[c] = ex;      /* vFlow.cpp:267 */
+        if (!o->serial) o->last_time[c] = et; /* vFlow.cpp:264 (serial: only after pooling, :790) */
+        o->cs_x[c] = ex;      /* vFlow.cpp:267 (serial: surfaceOfL, copied to cSurf, :591-610) */
         o->cs_y[c] = ey;
         o->cs_t[c] = et;
         double vx, vy;
@@ -356,6 +357,50 @@ int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
             scale_out[e] = sc;
         } else {
             r_true[e] = 0; theta_true[e] = 0; r_local[e] = 0; theta_local[e] = 0; scale_out[e] = 0;
+            o->flow_len[c] = 0;
+            o->flow_theta[c] = 0;
+        }
+        o->last_time[c] = et; /* vFlow.cpp:407 (serial :790) */
+    }
+    return 0;
+}
+
+void farms_oracle_set_serial(farms_oracle *o, int serial) { o->serial = serial != 0; }
+
+/* vFlow.cpp:531-556: the first line of the file only stamps lastEventTime, with
+ * its absolute time (t0 = time_, the subtraction starts with the next line). */
+void farms_oracle_serial_first(farms_oracle *o, int x, int y, uint32_t t_abs)
+{
+    if (x < 0 || x >= o->W || y < 0 || y >= o->H) return;
+    o->last_time[(size_t)x * o->H + y] = (double)t_abs;
+}
+
+int farms_oracle_pool_given(farms_oracle *o, const int32_t *x, const int32_t *y, const uint32_t *t_rel,
+                            const uint8_t *valid, const double *r_local, const double *theta_local, int64_t n,
+                            double *r_true, double *theta_true, int32_t *scale_out)
+{
+    const int W = o->W, H = o->H;
+    for (int64_t e = 0; e < n; ++e)
+        if (x[e] < 0 || x[e] >= W || y[e] < 0 || y[e] >= H) return -2;
+    for (int64_t e = 0; e < n; ++e) {
+        const int ex = x[e], ey = y[e];
+        const double et = (double)t_rel[e];
+        const size_t c = (size_t)ex * H + ey;
+        if (!o->serial) o->last_time[c] = et; /* vFlow.cpp:264 */
+        o->cs_x[c] = ex;
+        o->cs_y[c] = ey;
+        o->cs_t[c] = et;
+        if (valid[e]) { /* vFlow.cpp:315-362 with the given (length, theta) */
+            o->flow_len[c] = r_local[e];
+            o->flow_theta[c] = theta_local[e];
+            double gx, gy;
+            int sc;
+            compute_true_flow(o, ex, ey, et, &gx, &gy, &sc);
+            r_true[e] = sqrt(gy * gy + gx * gx);
+            theta_true[e] = atan2(gy, gx);
+            scale_out[e] = sc;
+        } else {
+            r_true[e] = 0; theta_true[e] = 0; scale_out[e] = 0;
             o->flow_len[c] = 0;
             o->flow_theta[c] = 0;
         }

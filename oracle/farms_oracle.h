@@ -51,6 +51,30 @@ int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
  * (zero on a fresh oracle). */
 void farms_oracle_seed_sae(farms_oracle *o, const int64_t *stamp);
 
+/* Serial mode: the per-event semantics of vFlowManager::run (src/vFlow.cpp:
+ * 465-826), the reference CLI's default.  Differences from runFileCopy:
+ *   - the first line of the file is not processed: it only sets
+ *     lastEventTime[x][y] to its absolute stamp (vFlow.cpp:531-556) and never
+ *     enters cSurf — farms_oracle_serial_first;
+ *   - lastEventTime[x][y] is written after pooling (:790), not before
+ *     (batch :264), so the pooled event's own cell is tested with the stamp of
+ *     the previous event at that pixel.
+ * cSurf is written before the fit in both modes (:591-610).  run() writes no
+ * output; the records here are for comparison only. */
+void farms_oracle_set_serial(farms_oracle *o, int serial);
+void farms_oracle_serial_first(farms_oracle *o, int x, int y, uint32_t t_abs);
+
+/* Pooling checker: the per-event loop with the local flows given instead of
+ * fitted.  valid[e] is the validity gate (vFlow.cpp:315) and r_local /
+ * theta_local the flow-surface values (:324-325) of event e, as produced by the
+ * path under test; the pooling (:952-1210) and the record's RTrue / ThetaTrue /
+ * scale (:365-381) are then computed here exactly as in farms_oracle_process.
+ * Given the same local flows, the per-scale sums, means and the chosen scale are
+ * those of the reference: the scale column must match bit for bit. */
+int farms_oracle_pool_given(farms_oracle *o, const int32_t *x, const int32_t *y, const uint32_t *t_rel,
+                            const uint8_t *valid, const double *r_local, const double *theta_local, int64_t n,
+                            double *r_true, double *theta_true, int32_t *scale);
+
 /* Number of pooling scales (floor(maxWindow/windowJump) + 1). */
 int farms_oracle_num_scales(const farms_oracle *o);
 

@@ -35,6 +35,11 @@ def load() -> ctypes.CDLL:
         lib.farms_oracle_num_scales.argtypes = [ctypes.c_void_p]
         lib.farms_oracle_seed_sae.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         lib.farms_oracle_seed_sae.restype = None
+        lib.farms_oracle_set_serial.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.farms_oracle_set_serial.restype = None
+        lib.farms_oracle_serial_first.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+        lib.farms_oracle_serial_first.restype = None
+        lib.farms_oracle_pool_given.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int64] + [ctypes.c_void_p] * 3
         _lib = lib
     return _lib
 
@@ -42,7 +47,8 @@ def load() -> ctypes.CDLL:
 class OracleFlow:
     """CPU vFlowManager batch loop: OracleFlow(height, width, filter_size, min_evts)."""
 
-    def __init__(self, height=320, width=320, filter_size=3, min_evts_on_plane=5, window_jump=5, max_window=50):
+    def __init__(self, height=320, width=320, filter_size=3, min_evts_on_plane=5, window_jump=5, max_window=50,
+                 serial=False):
         self._lib = load()
         h = ctypes.c_void_p()
         rc = self._lib.farms_oracle_create(int(width), int(height), int(filter_size), int(min_evts_on_plane),
@@ -50,6 +56,30 @@ class OracleFlow:
         if rc != 0:
             raise ValueError(f"farms_oracle_create failed ({rc})")
         self._h = h
+        if serial:
+            self._lib.farms_oracle_set_serial(self._h, 1)
+
+    def serial_first(self, x: int, y: int, t_abs: int) -> None:
+        """Serial mode: the file's first line only stamps lastEventTime (vFlow.cpp:531-556)."""
+        self._lib.farms_oracle_serial_first(self._h, int(x), int(y), int(t_abs) & 0xFFFFFFFF)
+
+    def pool_given(self, x, y, t_rel, valid, r_local, theta_local):
+        """Pooling with the local flows given (farms_oracle_pool_given): returns
+        r_true, theta_true, scale computed by the reference's pooling."""
+        x = np.ascontiguousarray(x, np.int32)
+        y = np.ascontiguousarray(y, np.int32)
+        t_rel = np.ascontiguousarray(t_rel, np.uint32)
+        valid = np.ascontiguousarray(valid, np.uint8)
+        r_local = np.ascontiguousarray(r_local, np.float64)
+        theta_local = np.ascontiguousarray(theta_local, np.float64)
+        n = int(x.shape[0])
+        rt, tt, sc = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
+        ptr = lambda a: ctypes.c_void_p(a.ctypes.data)
+        rc = self._lib.farms_oracle_pool_given(self._h, ptr(x), ptr(y), ptr(t_rel), ptr(valid), ptr(r_local),
+                                               ptr(theta_local), n, ptr(rt), ptr(tt), ptr(sc))
+        if rc != 0:
+            raise ValueError(f"farms_oracle_pool_given failed ({rc})")
+        return {"r_true": rt, "theta_true": tt, "scale": sc}
 
     def close(self):
         if self._h:

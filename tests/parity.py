@@ -2,7 +2,18 @@
 
 Bar (BASELINE.md §4, north_star): x/y/t/p and the validity flag bit-exact;
 RTrue/RLocal relative error <= 1e-4; ThetaTrue/ThetaLocal wrap-aware
-|dtheta| <= 1e-4 rad; scale-column mismatches counted and reported.
+|dtheta| <= 1e-4 rad.
+
+The scale column is an argmax over per-scale mean lengths, so an ulp anywhere
+in the summed lengths can flip it on a near tie.  Two checks pin it:
+  * pooling_check(): the oracle's pooling run on the GPU's own local flows
+    (oracle/farms_oracle.h, farms_oracle_pool_given).  Same inputs, same
+    summation order (vFlow.cpp:998-1021) -> the scale column must be identical.
+  * compare(): against the full oracle.  The only remaining difference is the
+    local flow itself, whose atan2/cos/sin come from ROCm's ocml on the GPU and
+    from glibc in the oracle; `local_ulp_events` counts the events whose Vx/Vy
+    differ bitwise, and a scale mismatch is accepted only where such an event
+    exists (scale_mismatch == 0 whenever the local flows are bitwise equal).
 """
 from __future__ import annotations
 
@@ -66,11 +77,47 @@ def compare(gpu, ref) -> dict:
     err = np.where(fin, err, np.where(same_nonfinite, 0.0, np.inf))
     rep["v_max_rel"] = float(err.max()) if err.size else 0.0
     rep["scale_mismatch"] = int(np.count_nonzero(_get(gpu, "scale")[both] != _get(ref, "scale")[both]))
+    # events whose local flow differs bitwise (libm ulps: ocml vs glibc atan2/cos/sin)
+    rep["local_ulp_events"] = int(np.count_nonzero((gx.view(np.int64) != rx.view(np.int64)) |
+                                                   (gy.view(np.int64) != ry.view(np.int64))))
     ok = all(rep[f"{c}_mismatch"] == 0 for c in ("x", "y", "t", "p")) and rep["valid_mismatch"] == 0
     ok = ok and rep["r_true_max_rel"] <= REL_TOL and rep["r_local_max_rel"] <= REL_TOL
     ok = ok and rep["theta_true_max_abs"] <= ANG_TOL and rep["theta_local_max_abs"] <= ANG_TOL
     ok = ok and rep["v_max_rel"] <= REL_TOL
+    ok = ok and (rep["scale_mismatch"] == 0 or rep["local_ulp_events"] > 0)
     rep["ok"] = bool(ok)
+    return rep
+
+
+def gate(vx, vy):
+    """Validity gate of vFlow.cpp:315 on the raw local flow."""
+    vx = np.asarray(vx, np.float64)
+    vy = np.asarray(vy, np.float64)
+    return ~np.isnan(vx) & ~np.isnan(vy) & (vx != 0) & (vy != 0)
+
+
+def pooling_check(gpu, height, width, window_jump=5, max_window=50, serial=False, first=None) -> dict:
+    """Run the oracle's pooling (vFlow.cpp:952-1210) on the GPU's own local flows
+    and compare: the scale column must match exactly, RTrue / ThetaTrue within
+    ocml-vs-glibc cos/sin ulps.  `first` = (x, y, t_abs) of a serial run's first
+    line (vFlow.cpp:531-556)."""
+    from oracle import OracleFlow
+
+    o = OracleFlow(height, width, 3, 5, window_jump, max_window, serial=serial)
+    if first is not None:
+        o.serial_first(*first)
+    valid = gate(_get(gpu, "vx"), _get(gpu, "vy"))
+    r = o.pool_given(_get(gpu, "x"), _get(gpu, "y"), np.asarray(_get(gpu, "t")).view(np.uint32), valid,
+                     _get(gpu, "r_local"), _get(gpu, "theta_local"))
+    o.close()
+    rep = {"pooled": int(valid.sum())}
+    rep["scale_mismatch"] = int(np.count_nonzero(np.asarray(_get(gpu, "scale"))[valid] != r["scale"][valid]))
+    e = rel_err(np.asarray(_get(gpu, "r_true"))[valid], r["r_true"][valid])
+    rep["r_true_max_rel"] = float(e.max()) if e.size else 0.0
+    d = wrap_diff(np.asarray(_get(gpu, "theta_true"))[valid], r["theta_true"][valid])
+    rep["theta_true_max_abs"] = float(np.nanmax(d)) if d.size else 0.0
+    rep["ok"] = bool(rep["scale_mismatch"] == 0 and rep["r_true_max_rel"] <= REL_TOL and
+                     rep["theta_true_max_abs"] <= ANG_TOL)
     return rep
 
 

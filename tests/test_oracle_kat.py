@@ -140,3 +140,60 @@ def test_out_of_sensor_event_rejected():
     with pytest.raises(ValueError):
         OracleFlow(10, 10, 3, 5).process(np.array([10], np.int32), np.array([0], np.int32),
                                          np.array([0], np.uint32), np.array([1], np.int32))
+
+
+def _bits(a):
+    return np.asarray(a, np.float64).view(np.int64)
+
+
+def test_pool_given_reproduces_the_oracle_pooling():
+    """farms_oracle_pool_given (the GPU pooling checker) fed the oracle's own
+    local flows reproduces the oracle's RTrue / ThetaTrue / scale bit for bit:
+    it is the same pooling (vFlow.cpp:952-1210), only the fit is skipped."""
+    import farms
+    from parity import gate
+
+    ev = farms.synth_config(2, 30_000)
+    x, y, t, p = ev.relative()
+    ref = OracleFlow(320, 320, 5, 5).process(x, y, t, p)
+    got = OracleFlow(320, 320, 5, 5).pool_given(x, y, t, gate(ref["vx"], ref["vy"]), ref["r_local"],
+                                                ref["theta_local"])
+    assert (ref["r_local"] > 0).sum() > 3000
+    for c in ("r_true", "theta_true"):
+        assert np.array_equal(_bits(got[c]), _bits(ref[c])), c
+    assert np.array_equal(got["scale"], ref["scale"])
+
+
+def test_serial_mode_semantics():
+    """vFlowManager::run (vFlow.cpp:465-826): lastEventTime is written after the
+    pooling (:790), so the pooled event's own cell is tested against the
+    previous event at its pixel; the first line only stamps lastEventTime
+    (:531-556).  A pixel that fires twice 100 us apart: in batch mode the own
+    cell always contributes (|dt| = 0); in serial mode only the second event's
+    own cell does (its previous stamp is 100 us old), the first event's own cell
+    carries the t = 0 'never visited' stamp, 5000 us away."""
+    a, b = 2e-3, 1e-3
+    x, y, t, p = ramp(24, 24, a, b, t0=5000)
+    i = int(np.flatnonzero((x == 12) & (y == 12))[0])
+    # the same pixel again, 100 us later, appended at the end of the stream
+    x2 = np.append(x, x[i]).astype(np.int32)
+    y2 = np.append(y, y[i]).astype(np.int32)
+    t2 = np.append(t, t.max() + 100).astype(np.uint32)
+    p2 = np.ones(x2.size, np.int32)
+    batch = OracleFlow(24, 24, 3, 3).process(x2, y2, t2, p2)
+    ser = OracleFlow(24, 24, 3, 3, serial=True)
+    s = ser.process(x2, y2, t2, p2)
+    # the fit reads cSurf, written before the fit in both modes: identical local flows
+    assert np.array_equal(_bits(batch["vx"]), _bits(s["vx"]))
+    assert np.array_equal(_bits(batch["vy"]), _bits(s["vy"]))
+    # an isolated event (no neighbour within 500 us) pools only itself in batch
+    # mode and nothing in serial mode: scale 0 either way, global = its own flow
+    # (vFlow.cpp:1085-1094) — so compare the events whose pooling differs
+    diff = np.flatnonzero(_bits(batch["r_true"]) != _bits(s["r_true"]))
+    assert diff.size > 0  # the own-cell stamp changes some poolings
+    # first line of a serial run: lastEventTime[x][y] = absolute t, no SAE entry
+    o = OracleFlow(24, 24, 3, 3, serial=True)
+    o.serial_first(3, 4, 123456)
+    one = o.process(np.array([3], np.int32), np.array([4], np.int32), np.array([0], np.uint32),
+                    np.array([1], np.int32))
+    assert one["r_local"][0] == 0  # a lone event: DET < 1

@@ -26,7 +26,8 @@
 // these two sweeps reproduce the sequential semantics exactly.
 //
 // Numerics: fp64 throughout, compiled with -ffp-contract=off (no FMA), with the
-// reference's (and Eigen 3.4's) evaluation order for the fit; see DESIGN.md §3.
+// reference's (and Eigen 3.4's) evaluation order for the fit, and correctly
+// rounded atan2 / sin / cos (farms_libm.h); see DESIGN.md §3.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -40,6 +41,7 @@
 #include <cstdlib>
 
 #include "../../include/farms_hip.h"
+#include "farms_libm.h"
 
 namespace {
 
@@ -486,9 +488,9 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = atan2(r0, r1);
-    vx_out = speed * cos(angle);
-    vy_out = speed * sin(angle);
+    const double angle = farms_libm::cr_atan2(r0, r1);
+    vx_out = speed * farms_libm::cr_cos(angle);
+    vy_out = speed * farms_libm::cr_sin(angle);
 }
 
 // Local plane fit of one event with fRad known at compile time (the common
@@ -661,9 +663,9 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = atan2(r0, r1);
-    vx_out = speed * cos(angle);
-    vy_out = speed * sin(angle);
+    const double angle = farms_libm::cr_atan2(r0, r1);
+    vx_out = speed * farms_libm::cr_cos(angle);
+    vy_out = speed * farms_libm::cr_sin(angle);
 }
 
 // Validity gate, flow-surface value and record of one fitted event.
@@ -678,10 +680,10 @@ __device__ __forceinline__ void fit_store(const Ctx &c, int e, double vx, double
     double L = 0.0, th = 0.0;
     if (ok) {
         L = sqrt(vx * vx + vy * vy);
-        th = atan2(vy, vx);
+        th = farms_libm::cr_atan2(vy, vx);
         f.L = L;
-        f.Lc = L * cos(th);
-        f.Ls = L * sin(th);
+        f.Lc = L * farms_libm::cr_cos(th);
+        f.Ls = L * farms_libm::cr_sin(th);
     } else {
         f.L = 0.0; f.Lc = 0.0; f.Ls = 0.0;
     }
@@ -914,9 +916,9 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = atan2(r0, r1);
-    vx_out = speed * cos(angle);
-    vy_out = speed * sin(angle);
+    const double angle = farms_libm::cr_atan2(r0, r1);
+    vx_out = speed * farms_libm::cr_cos(angle);
+    vy_out = speed * farms_libm::cr_sin(angle);
 }
 
 // Variant that keeps the union: every lane writes the stamps of its union
@@ -1088,9 +1090,9 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = atan2(r0, r1);
-    vx_out = speed * cos(angle);
-    vy_out = speed * sin(angle);
+    const double angle = farms_libm::cr_atan2(r0, r1);
+    vx_out = speed * farms_libm::cr_cos(angle);
+    vy_out = speed * farms_libm::cr_sin(angle);
 }
 
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
@@ -1266,9 +1268,9 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
         }
         inliers = (int)wave_sum_i64(inl);
         const double speed = 1.0 / dtdp;
-        const double angle = atan2(r0, r1);
-        dtdx = speed * cos(angle);
-        dtdy = speed * sin(angle);
+        const double angle = farms_libm::cr_atan2(r0, r1);
+        dtdx = speed * farms_libm::cr_cos(angle);
+        dtdy = speed * farms_libm::cr_sin(angle);
     }
     if (lane == 0) {
         double vx = 0.0, vy = 0.0;
@@ -1835,7 +1837,7 @@ __global__ void k_true_polar(Ctx c) {
     if (x < c.own_lo || x >= c.own_hi) return;
     const double gx = c.r_true[e], gy = c.th_true[e];
     c.r_true[e] = sqrt(gy * gy + gx * gx);
-    c.th_true[e] = atan2(gy, gx);
+    c.th_true[e] = farms_libm::cr_atan2(gy, gx);
 }
 
 // ---------------------------------------------------------------------------

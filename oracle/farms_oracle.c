@@ -30,6 +30,11 @@
 struct farms_oracle {
     int W, H;
     int serial; /* vFlowManager::run semantics (farms_oracle.h) */
+    /* libm of the path: glibc's atan2 / sin / cos (the reference's) unless a
+     * test swaps in another implementation (farms_oracle_set_libm) */
+    double (*f_atan2)(double, double);
+    double (*f_sin)(double);
+    double (*f_cos)(double);
     int frad, plane_size, min_inliers;
     int window_jump, max_window, nscales;
     /* cSurf (vFlow.h:51): stored Event x, y, stamp per cell, x-major (EventMatrix.h:32-33) */
@@ -64,6 +69,9 @@ int farms_oracle_create(int width, int height, int filter_size, int min_inliers,
     o->window_jump = window_jump;
     o->max_window = max_window;
     o->nscales = nscales;
+    o->f_atan2 = atan2;
+    o->f_sin = sin;
+    o->f_cos = cos;
     size_t cells = (size_t)width * (size_t)height;
     o->cs_x = (int *)calloc(cells, sizeof(int));
     o->cs_y = (int *)calloc(cells, sizeof(int));
@@ -150,7 +158,7 @@ static double eigen_det3_partialpivlu(const double ata[9])
 /* n rows: X[k], Y[k] (stored event coords), T[k] (stored stamp, double).
  * cen = the current event.  Returns the inlier count, writes dtdx/dtdy only when
  * DET >= 1 (vFlow.cpp:1323 returns before touching them otherwise). */
-static int compute_grads(int n, const double *X, const double *Y, const double *T,
+static int compute_grads(const farms_oracle *o, int n, const double *X, const double *Y, const double *T,
                          double cen_x, double cen_y, double cen_t, double *dtdy, double *dtdx,
                          double *Yt /* scratch n */)
 {
@@ -219,9 +227,9 @@ static int compute_grads(int n, const double *X, const double *Y, const double *
         if (fabs(planedt - actualdt) < dtdp / 2 && Yt[k] > 0) inliers++;
     }
     double speed = 1.0 / dtdp;
-    double angle = atan2(abc[0], abc[1]);
-    *dtdx = speed * cos(angle);
-    *dtdy = speed * sin(angle);
+    double angle = o->f_atan2(abc[0], abc[1]);
+    *dtdx = speed * o->f_cos(angle);
+    *dtdy = speed * o->f_sin(angle);
     return inliers;
 }
 
@@ -266,7 +274,7 @@ static void compute_local_flow(farms_oracle *o, int ex, int ey, double et, doubl
             Ts[k] = o->cs_t[c];
             ++k;
         }
-    int inl = compute_grads(k, Xs, Ys, Ts, ex, ey, et, &dtdy, &dtdx, Yt);
+    int inl = compute_grads(o, k, Xs, Ys, Ts, ex, ey, et, &dtdy, &dtdx, Yt);
     if (inl >= o->min_inliers) { *vx = dtdx; *vy = dtdy; } /* vFlow.cpp:934-942 */
 }
 
@@ -289,8 +297,8 @@ static void compute_true_flow(farms_oracle *o, int x, int y, double te, double *
                 double L = o->flow_len[c];
                 if (L > 0 && fabs(te - o->last_time[c]) < KILL_OLD_FLOW_TIME) {
                     len = len + L;
-                    sxv = sxv + L * cos(o->flow_theta[c]);
-                    syv = syv + L * sin(o->flow_theta[c]);
+                    sxv = sxv + L * o->f_cos(o->flow_theta[c]);
+                    syv = syv + L * o->f_sin(o->flow_theta[c]);
                     num++;
                 }
             }
@@ -308,8 +316,8 @@ static void compute_true_flow(farms_oracle *o, int x, int y, double te, double *
         *scale = maxi * o->window_jump;
     } else { /* vFlow.cpp:1085-1094 */
         size_t c = (size_t)x * H + y;
-        *gx = o->flow_len[c] * cos(o->flow_theta[c]);
-        *gy = o->flow_len[c] * sin(o->flow_theta[c]);
+        *gx = o->flow_len[c] * o->f_cos(o->flow_theta[c]);
+        *gy = o->flow_len[c] * o->f_sin(o->flow_theta[c]);
         *scale = 0;
     }
 }
@@ -344,14 +352,14 @@ int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
         vy_out[e] = vy;
         if (!isnan(fabs(vx)) && !isnan(fabs(vy)) && vx != 0 && vy != 0) { /* vFlow.cpp:315 */
             double length = sqrt(vx * vx + vy * vy);
-            double theta = atan2(vy, vx);
+            double theta = o->f_atan2(vy, vx);
             o->flow_len[c] = length;
             o->flow_theta[c] = theta;
             double gx, gy;
             int sc;
             compute_true_flow(o, ex, ey, et, &gx, &gy, &sc);
             r_true[e] = sqrt(gy * gy + gx * gx);
-            theta_true[e] = atan2(gy, gx);
+            theta_true[e] = o->f_atan2(gy, gx);
             r_local[e] = length;
             theta_local[e] = theta;
             scale_out[e] = sc;
@@ -366,6 +374,14 @@ int farms_oracle_process(farms_oracle *o, const int32_t *x, const int32_t *y,
 }
 
 void farms_oracle_set_serial(farms_oracle *o, int serial) { o->serial = serial != 0; }
+
+void farms_oracle_set_libm(farms_oracle *o, double (*f_atan2)(double, double), double (*f_sin)(double),
+                           double (*f_cos)(double))
+{
+    o->f_atan2 = f_atan2 ? f_atan2 : atan2;
+    o->f_sin = f_sin ? f_sin : sin;
+    o->f_cos = f_cos ? f_cos : cos;
+}
 
 /* vFlow.cpp:531-556: the first line of the file only stamps lastEventTime, with
  * its absolute time (t0 = time_, the subtraction starts with the next line). */
@@ -397,7 +413,7 @@ int farms_oracle_pool_given(farms_oracle *o, const int32_t *x, const int32_t *y,
             int sc;
             compute_true_flow(o, ex, ey, et, &gx, &gy, &sc);
             r_true[e] = sqrt(gy * gy + gx * gx);
-            theta_true[e] = atan2(gy, gx);
+            theta_true[e] = o->f_atan2(gy, gx);
             scale_out[e] = sc;
         } else {
             r_true[e] = 0; theta_true[e] = 0; scale_out[e] = 0;

@@ -75,6 +75,14 @@ int farms_oracle_pool_given(farms_oracle *o, const int32_t *x, const int32_t *y,
                             const uint8_t *valid, const double *r_local, const double *theta_local, int64_t n,
                             double *r_true, double *theta_true, int32_t *scale);
 
+/* The libm of the path.  Default: glibc's atan2 / sin / cos, as the reference
+ * calls them (vFlow.cpp:325, 366, 1007-1008, 1375-1377) — this is the
+ * reference.  Tests may swap in the HIP path's correctly rounded versions
+ * (csrc/farms_libm.h, host build) to check the rest of the GPU arithmetic bit
+ * for bit; NULL restores glibc's. */
+void farms_oracle_set_libm(farms_oracle *o, double (*f_atan2)(double, double), double (*f_sin)(double),
+                           double (*f_cos)(double));
+
 /* Number of pooling scales (floor(maxWindow/windowJump) + 1). */
 int farms_oracle_num_scales(const farms_oracle *o);
 

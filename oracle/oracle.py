@@ -39,16 +39,30 @@ def load() -> ctypes.CDLL:
         lib.farms_oracle_set_serial.restype = None
         lib.farms_oracle_serial_first.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         lib.farms_oracle_serial_first.restype = None
+        lib.farms_oracle_set_libm.argtypes = [ctypes.c_void_p] * 4
+        lib.farms_oracle_set_libm.restype = None
         lib.farms_oracle_pool_given.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int64] + [ctypes.c_void_p] * 3
         _lib = lib
     return _lib
+
+
+_cr = None
+
+
+def _cr_libm() -> ctypes.CDLL:
+    global _cr
+    if _cr is None:
+        path = os.path.join(os.path.dirname(HERE), "aperture-robust-multiscale-optical-flow_amd", "build",
+                            "libfarms_libm_check.so")
+        _cr = ctypes.CDLL(path)
+    return _cr
 
 
 class OracleFlow:
     """CPU vFlowManager batch loop: OracleFlow(height, width, filter_size, min_evts)."""
 
     def __init__(self, height=320, width=320, filter_size=3, min_evts_on_plane=5, window_jump=5, max_window=50,
-                 serial=False):
+                 serial=False, libm="glibc"):
         self._lib = load()
         h = ctypes.c_void_p()
         rc = self._lib.farms_oracle_create(int(width), int(height), int(filter_size), int(min_evts_on_plane),
@@ -58,6 +72,14 @@ class OracleFlow:
         self._h = h
         if serial:
             self._lib.farms_oracle_set_serial(self._h, 1)
+        if libm == "cr":
+            # the HIP path's correctly rounded atan2 / sin / cos (host build of
+            # csrc/farms_libm.h): checks the rest of the GPU arithmetic bitwise
+            cr = _cr_libm()
+            self._lib.farms_oracle_set_libm(self._h, *[ctypes.cast(getattr(cr, f), ctypes.c_void_p)
+                                                       for f in ("farms_cr_atan2", "farms_cr_sin", "farms_cr_cos")])
+        elif libm != "glibc":
+            raise ValueError("libm must be 'glibc' (the reference) or 'cr'")
 
     def serial_first(self, x: int, y: int, t_abs: int) -> None:
         """Serial mode: the file's first line only stamps lastEventTime (vFlow.cpp:531-556)."""

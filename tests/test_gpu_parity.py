@@ -1,10 +1,18 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle.
 
 Oracle status: "parity unpinned" (no reference fixtures exist; the reference
-cannot be built here — see DESIGN.md §4).  Tolerances: tests/parity.py
-(indices / polarity / validity bit-exact, r and theta within 1e-4).
+cannot be built here — see DESIGN.md §4).  Every stream is checked three ways:
+  * against the oracle with glibc's libm (the reference): the bar of
+    tests/parity.py (indices / polarity / validity bit-exact, r and theta
+    within 1e-4); the libm residual is counted;
+  * against the oracle with the HIP path's correctly rounded atan2 / sin / cos
+    (farms_oracle_set_libm): every column bit for bit — the fit, the gate and
+    the pooling arithmetic of the GPU are the reference's;
+  * pooling_check: the reference pooling over the GPU's own local flows gives
+    the identical scale column.
 """
 import numpy as np
+import torch  # noqa: F401  (its HIP runtime loads before libfarms_hip.so: farms.load_hip_library)
 import pytest
 
 import farms
@@ -16,23 +24,33 @@ pytestmark = pytest.mark.gpu
 SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720)}
 
 
+def oracles(x, y, t, p, height, width, fs, inl=5, jump=5, maxw=50):
+    """Records of the reference restatement (glibc libm) and of the same
+    restatement with the HIP path's correctly rounded libm."""
+    r = OracleFlow(height, width, fs, inl, jump, maxw).process(x, y, t, p)
+    rc = OracleFlow(height, width, fs, inl, jump, maxw, libm="cr").process(x, y, t, p)
+    return r, rc
+
+
 def run_pair(ev, width, height, fs, inl=5, jump=5, maxw=50, **kw):
     x, y, t, p = ev.relative()
     with farms.FlowManager(height, width, fs, inl, window_jump=jump, max_window=maxw, **kw) as fm:
         g = fm.process(x, y, t, p)
-    r = OracleFlow(height, width, fs, inl, jump, maxw).process(x, y, t, p)
-    return g, r
+    return (g,) + oracles(x, y, t, p, height, width, fs, inl, jump, maxw)
 
 
-def assert_parity(g, r, height, width, jump=5, maxw=50):
-    """The bar of tests/parity.py, plus the pooling pinned exactly: the oracle's
-    pooling over the GPU's own local flows gives the identical scale column."""
+def assert_parity(g, r, height, width, jump=5, maxw=50, rc=None):
+    """The bar of tests/parity.py against the reference restatement, the scale
+    column pinned exactly by pooling_check, and (rc) every column bitwise equal
+    to the restatement run with the GPU's correctly rounded libm."""
     rep = compare(g, r)
     pc = pooling_check(g, height, width, jump, maxw)
     print(rep, pc)
     assert rep["ok"], rep
     assert pc["ok"], pc
     assert pc["scale_mismatch"] == 0, pc
+    if rc is not None:
+        assert bitwise_equal(g, rc), compare(g, rc)
     return rep
 
 
@@ -40,16 +58,16 @@ def assert_parity(g, r, height, width, jump=5, maxw=50):
 def test_configs_vs_oracle(cfg, n, fs):
     W, H = SENSOR[cfg]
     ev = farms.synth_config(cfg, n)
-    g, r = run_pair(ev, W, H, fs)
-    rep = assert_parity(g, r, H, W)
+    g, r, rc = run_pair(ev, W, H, fs)
+    rep = assert_parity(g, r, H, W, rc=rc)
     assert rep["valid_ref"] > n // 20  # the stream really exercises pooling
 
 
 def test_config4_stream_vs_oracle():
     """BASELINE config 4's own stream (seed 0x5EED0004, fs 7, 11 scales)."""
     ev = farms.synth_config(4, 150_000)
-    g, r = run_pair(ev, 1280, 720, 7)
-    rep = assert_parity(g, r, 720, 1280)
+    g, r, rc = run_pair(ev, 1280, 720, 7)
+    rep = assert_parity(g, r, 720, 1280, rc=rc)
     assert rep["valid_ref"] > 150_000 // 20
 
 
@@ -69,16 +87,16 @@ def test_short_wide_sensor_double_visits():
     x[:50] = W - 1  # last column: the window runs past the end of the surfaces
     with farms.FlowManager(H, W, 3, 3) as fm:
         g = fm.process(x, y, t, p)
-    r = OracleFlow(H, W, 3, 3).process(x, y, t, p)
-    rep = assert_parity(g, r, H, W)
+    r, rc = oracles(x, y, t, p, H, W, 3, 3)
+    rep = assert_parity(g, r, H, W, rc=rc)
     assert rep["valid_ref"] > 1000
 
 
 def test_three_scales_vs_oracle():
     """BASELINE config 5 shape: fs=7 with scales {0,25,50}."""
     ev = farms.synth_config(5, 120_000)
-    g, r = run_pair(ev, 1280, 720, 7, jump=25, maxw=50)
-    assert_parity(g, r, 720, 1280, 25, 50)
+    g, r, rc = run_pair(ev, 1280, 720, 7, jump=25, maxw=50)
+    assert_parity(g, r, 720, 1280, 25, 50, rc=rc)
     assert set(np.unique(g.scale)) <= {0, 25, 50}
 
 
@@ -127,8 +145,8 @@ def test_unsorted_timestamps_vs_oracle():
     t = t.astype(np.uint32)
     with farms.FlowManager(320, 320, 5, 5) as fm:
         g = fm.process(x, y, t, p)
-    r = OracleFlow(320, 320, 5, 5).process(x, y, t, p)
-    assert_parity(g, r, 320, 320)
+    r, rc = oracles(x, y, t, p, 320, 320, 5, 5)
+    assert_parity(g, r, 320, 320, rc=rc)
 
 
 def test_edges_hot_pixel_and_filter_sizes():
@@ -148,8 +166,8 @@ def test_edges_hot_pixel_and_filter_sizes():
     for fs, inl in [(1, 5), (2, 3), (4, 5), (5, 0), (6, 7), (7, 4), (9, 10)]:
         with farms.FlowManager(H, W, fs, inl) as fm:
             g = fm.process(x, y, t, p)
-        r = OracleFlow(H, W, fs, inl).process(x, y, t, p)
-        assert_parity(g, r, H, W)
+        r, rc = oracles(x, y, t, p, H, W, fs, inl)
+        assert_parity(g, r, H, W, rc=rc)
 
 
 def test_tall_sensor_and_tiny_sensor():
@@ -162,8 +180,8 @@ def test_tall_sensor_and_tiny_sensor():
         p = np.ones(n, np.int32)
         with farms.FlowManager(H, W, 3, 3) as fm:
             g = fm.process(x, y, t, p)
-        r = OracleFlow(H, W, 3, 3).process(x, y, t, p)
-        assert_parity(g, r, H, W)
+        r, rc = oracles(x, y, t, p, H, W, 3, 3)
+        assert_parity(g, r, H, W, rc=rc)
 
 
 def test_empty_and_single_event():
@@ -230,6 +248,6 @@ def test_full_size_stream_properties():
     k = 100_000
     g = {c: v for c, v in zip(farms.COLUMNS[:4], (x[:k], y[:k], t[:k].astype(np.int32), p[:k]))}
     g.update({c: outs[0][c][:k].cpu().numpy() for c in farms.COLUMNS[4:]})
-    r = OracleFlow(720, 1280, 5, 5).process(x[:k], y[:k], t[:k], p[:k])
-    assert_parity(g, r, 720, 1280)
+    r, rc = oracles(x[:k], y[:k], t[:k], p[:k], 720, 1280, 5, 5)
+    assert_parity(g, r, 720, 1280, rc=rc)
     assert int((outs[0]["r_local"] > 0).sum()) > n // 4  # most of the stream is pooled

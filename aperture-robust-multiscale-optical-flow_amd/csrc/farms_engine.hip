@@ -1527,6 +1527,12 @@ __device__ __forceinline__ double wave_max(double v) {
 // s_row the non-empty segments in order {row, candidate index - flattened
 // index}; s_con the staged contributors {ref, kind | k0 << 8}; s_val / s_k0
 // the values {L, L cos, L sin} and k0 of 64 staged entries.
+#ifndef FARMS_POOL_STOP
+#define FARMS_POOL_STOP 0  // ablation aid (variants only): 1 row setup, 2 + phase A, 3 all but the phase B folds
+#endif
+#ifndef FARMS_POOL_UNROLL
+#define FARMS_POOL_UNROLL 8  // phase B entries per loop trip (4 or 8; 64 must be a multiple)
+#endif
 template <int K>
 __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
                                            uint64_t *s_start, int2 *s_row, uint2 *s_con, double *s_val,
@@ -1625,6 +1631,10 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const int total = carry;
+#if FARMS_POOL_STOP == 1
+    if (lane == 0) c.scale[e] = total;  // ablation: row setup only
+    return;
+#endif
 
     // ---- phase A: stage contributors with rank in [pass*cap, (pass+1)*cap) in
     // LDS; returns the total number of contributors
@@ -1724,6 +1734,10 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
             __builtin_amdgcn_wave_barrier();
         }
         ncon_total = collect(pass);
+#if FARMS_POOL_STOP == 2
+        if (lane == 0) c.scale[e] = ncon_total;  // ablation: row setup + phase A
+        return;
+#endif
         npass = ncon_total > kPoolCap ? (ncon_total + kPoolCap - 1) / kPoolCap : 1;
         const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
         // entry b0 + lane of the sub-batch at b0: its values and k0 (K: in no scale)
@@ -1748,16 +1762,25 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if (b0 + 64 < nb) fetch(b0 + 64);
-            const int cnt = min(64, nb - b0);
+            const int cnt = __builtin_amdgcn_readfirstlane(min(64, nb - b0));  // wave-uniform
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+            // Member entries are added as fma(v, 1, acc) = acc + v (one
+            // rounding), non-members as fma(v, 0, acc) = acc + (+-0) = acc: acc
+            // starts at +0 and a round-to-nearest sum is -0 only when both
+            // addends are, so acc is never -0 and the masked fold is bitwise
+            // the reference's conditional one (valid flows are finite).  The
+            // multiplier is off the dependency chain: one fma per entry on it.
 #pragma unroll 1
-            for (int r = 0; r < cnt; r += 4) {  // entries past cnt have k0 = K: no scale adds them
-                const uint32_t k4 = k4p[r >> 2];
+            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // entries past cnt have k0 = K: no scale adds them
+                uint32_t kw[FARMS_POOL_UNROLL / 4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int k0 = (int)((k4 >> (8 * u)) & 0xFFu);
+                for (int u = 0; u < FARMS_POOL_UNROLL / 4; ++u) kw[u] = k4p[(r >> 2) + u];
+#pragma unroll
+                for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
+                    const int k0 = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
                     const double v = s_val[3 * (r + u) + grp];
-                    acc = kk >= k0 ? acc + v : acc;
+                    const double m = kk >= k0 ? 1.0 : 0.0;
+                    acc = __builtin_fma(v, m, acc);
                 }
             }
         }

@@ -31,14 +31,20 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
-#include <cstdlib>
 
 #include "../../include/farms_hip.h"
 #include "farms_libm.h"
@@ -152,6 +158,11 @@ struct Ctx {
     int NB, C2;            // ring size, events per pooling chunk
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
+    // serial mode (vFlowManager::run, vFlow.cpp:465-826): per event, the stamp
+    // its pixel's lastEventTime holds while the event is pooled (written only
+    // after pooling, :790): the previous event's there, else the stamp before
+    // the call.  nullptr in batch mode.
+    const uint32_t *tprev;
     // outputs
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
     int32_t *scale;
@@ -248,7 +259,7 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
     iota[e] = e;
 }
 
-__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *PT) {
+__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *PT, uint32_t *tprev) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c.n) return;
     const int e = c.P[k];
@@ -257,6 +268,11 @@ __global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *
     PT[k] = make_int2(e, (int)c.t[e]);
     const bool first = !(k > 0 && c.skey[k - 1] == q), last = !(k + 1 < c.n && c.skey[k + 1] == q);
     prev[e] = first ? -1 : c.P[k - 1];
+    // serial mode: lastEventTime[x][y] while e is pooled.  Before the call it
+    // is the flow snapshot's stamp (the last event at q, 0 if none, or the
+    // first line's stamp set by farms_serial_first); the pooling chain only
+    // advances fsnap after prep.
+    if (tprev) tprev[e] = first ? c.fsnap[q].t : c.t[c.P[k - 1]];
     next[e] = last ? INT_MAX : c.P[k + 1];
     if (first) c.pcur[q] = k;  // the pooling chain's run bounds of the cell
     if (last) c.pend[q] = k;
@@ -1543,6 +1559,10 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     const int W = c.W, H = c.H, M = c.M, J = c.J;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
     const int WHs = (int)c.WHs;
+    // serial mode: the own cell is pooled with the stamp its lastEventTime still
+    // holds (the previous event's), not the event's own (vFlow.cpp:790 vs :264)
+    const uint32_t own_lin = c.tprev ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
+    const uint32_t own_tprev = c.tprev ? c.tprev[e] : 0u;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= 127
@@ -1676,6 +1696,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
                     const FlowCell fe = c.evf[sev];
                     ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)sev;
                 }
+                if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
                 // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
                 const int64_t dt = (int64_t)teu - (int64_t)tq;
                 if (ok && (uint64_t)(dt + 499) < 999u) {
@@ -1853,9 +1874,9 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
 // owned) event: k_pool leaves (Gx, Gy) in the r_true / theta_true columns.
-__global__ void k_true_polar(Ctx c) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= c.n || !c.valid[e]) return;
+__global__ void k_true_polar(Ctx c, int e0, int e1) {
+    const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= e1 || !c.valid[e]) return;
     const int x = c.x[e];
     if (x < c.own_lo || x >= c.own_hi) return;
     const double gx = c.r_true[e], gy = c.th_true[e];
@@ -1988,6 +2009,9 @@ struct farms_handle {
     uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
     int32_t *iota = nullptr, *P = nullptr, *pos = nullptr, *prev = nullptr, *next = nullptr;
     int32_t *Q = nullptr;
+    uint32_t *tprev = nullptr;  // serial mode only
+    int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
+    uint32_t first_t = 0;
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     int tile_bits = 0;
     uint8_t *valid = nullptr;
@@ -2006,6 +2030,13 @@ struct farms_handle {
     hipEvent_t ev[8] = {};
     std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
     farms_stats stats{};
+    // host-array path (farms_process): pinned staging of inputs (16 B/event)
+    // and records (52 B/event), a copy stream for the record downloads, one
+    // completion event per pooling super-chunk
+    uint8_t *pin_in = nullptr, *pin_out = nullptr;
+    int64_t pin_cap = 0;
+    hipStream_t s_copy = nullptr;
+    std::vector<hipEvent_t> copy_ev;
 };
 
 namespace {
@@ -2025,7 +2056,7 @@ void dfree(T *&p) {
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->pos); dfree(h->prev); dfree(h->next);
-    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
+    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted); dfree(h->tprev);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2052,7 +2083,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
-        (rc = dalloc(&h->ctmax, nch))) {
+        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap)))) {
         free_workspace(h);
         return rc;
     }
@@ -2079,6 +2110,7 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
+    h->first_q = -1;
     return FARMS_OK;
 }
 
@@ -2145,9 +2177,13 @@ int ensure_sync_events(farms_handle *h, size_t count) {
     return FARMS_OK;
 }
 
-// The whole per-event loop for n device-resident events.
+// The whole per-event loop for n device-resident events.  on_super (may be
+// null) is called as soon as the work of pooling super-chunk S (events [p0,
+// p1)) is enqueued, with the event that marks its records final on the device:
+// the host-array path starts the download of those records there.
+typedef std::function<int(int S, int p0, int p1, hipEvent_t done)> super_hook;
 int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
-             int64_t n64, farms_records *dout) {
+             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr) {
     const int n = (int)n64;
     hipStream_t s = h->stream;
     Ctx c{};
@@ -2161,6 +2197,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.pcur = h->pcur; c.pend = h->pend;
+    c.tprev = h->prm.serial ? h->tprev : nullptr;
     c.bm_ring = h->bm_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
@@ -2205,7 +2242,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
                                               end_bit_for(h->WH), s));
     HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
-    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next, h->PT);
+    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next, h->PT,
+                       h->prm.serial ? h->tprev : nullptr);
     {
         int cb = 1;
         while ((1 << cb) < n_pool_chunks) ++cb;
@@ -2284,7 +2322,13 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
         pl(c, p0, p1, sp);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
+        // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
+        hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
         HIPCHK(hipEventRecord(ev_pool(S), sp));
+        if (on_super) {
+            int rc = (*on_super)(S, p0, p1, ev_pool(S));
+            if (rc) return rc;
+        }
     }
     while (fit_enqueued < n_fit_chunks) {
         int rc = enqueue_fit(fit_enqueued++);
@@ -2298,7 +2342,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
     }
-    if (n_super > 0) hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (h->counting) {
         HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 5, s));
@@ -2458,6 +2501,10 @@ extern "C" int farms_destroy(farms_handle *h) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);
     for (auto &ev : h->sync_ev) (void)hipEventDestroy(ev);
+    for (auto &ev : h->copy_ev) (void)hipEventDestroy(ev);
+    if (h->s_copy) { (void)hipStreamSynchronize(h->s_copy); (void)hipStreamDestroy(h->s_copy); }
+    if (h->pin_in) (void)hipHostFree(h->pin_in);
+    if (h->pin_out) (void)hipHostFree(h->pin_out);
     if (h->s_pool) (void)hipStreamDestroy(h->s_pool);
     if (h->s_chain) (void)hipStreamDestroy(h->s_chain);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -2498,6 +2545,14 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
                                     h->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
     (void)hipFree(d);
+    // serial mode: the first line stamps lastEventTime without entering the SAE
+    // (vFlow.cpp:556); it shows until an event fires at that pixel
+    if (h->first_q >= 0 && out[h->first_q] == 0.0) {
+        FlowCell f{};
+        if (hipMemcpy(&f, h->fsnap + (h->first_q - (int64_t)h->X0 * h->H), sizeof(f), hipMemcpyDeviceToHost) == hipSuccess &&
+            f.t == h->first_t)
+            out[h->first_q] = (double)h->first_t;
+    }
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
     return FARMS_OK;
 }
@@ -2547,6 +2602,21 @@ extern "C" int farms_seed_sae(farms_handle *h, const int64_t *d_stamp) {
     return FARMS_OK;
 }
 
+extern "C" int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_t t_abs) {
+    if (!h) return fail(FARMS_EINVAL, "null handle");
+    if (!h->prm.serial) return fail(FARMS_EINVAL, "farms_serial_first needs a serial-mode handle");
+    if (x < h->X0 || x >= h->X0 + h->WR || y < 0 || y >= h->H) return fail(FARMS_EINVAL, "event outside the sensor");
+    HIPCHK(hipSetDevice(h->prm.device));
+    const int64_t q = (int64_t)(x - h->X0) * h->H + y;
+    // lastEventTime[x][y] = t_abs (vFlow.cpp:556): the stamp field of the flow
+    // snapshot, whose length stays 0 (the cell has no flow yet)
+    HIPCHK(hipMemcpy(reinterpret_cast<uint8_t *>(h->fsnap + q) + offsetof(FlowCell, t), &t_abs, sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+    h->first_q = (int64_t)x * h->H + y;
+    h->first_t = t_abs;
+    return FARMS_OK;
+}
+
 extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
                                     const uint32_t *d_t, const int32_t *d_p, int64_t n, farms_records *d_out) {
     if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
@@ -2561,6 +2631,38 @@ extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const i
     return run_core(h, d_x, d_y, d_t, d_p, n, d_out);
 }
 
+namespace {
+
+int host_threads() {
+    // FARMS_HOST_THREADS: host threads of the staging copies (default 8)
+    const char *v = getenv("FARMS_HOST_THREADS");
+    const int t = v ? atoi(v) : 8;
+    return std::max(1, std::min(t, 64));
+}
+
+int ensure_pinned(farms_handle *h, int64_t n) {
+    if (n <= h->pin_cap) return FARMS_OK;
+    if (h->pin_in) (void)hipHostFree(h->pin_in);
+    if (h->pin_out) (void)hipHostFree(h->pin_out);
+    h->pin_in = h->pin_out = nullptr;
+    h->pin_cap = 0;
+    HIPCHK(hipHostMalloc((void **)&h->pin_in, (size_t)n * 16, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void **)&h->pin_out, (size_t)n * 52, hipHostMallocDefault));
+    h->pin_cap = n;
+    return FARMS_OK;
+}
+
+}  // namespace
+
+// Host arrays in and out (the CLI path, vFlow.cpp:214-416 timed region).
+//   upload: host threads copy slices of x, y, t, p into pinned staging and each
+//     enqueues its slice's DMA right away (copies and DMA overlap);
+//   compute: run_core, unchanged;
+//   download: as each pooling super-chunk's records become final on the device
+//     (run_core's hook), its seven columns are DMAed into pinned staging on a
+//     copy stream while later super-chunks compute, and host threads move them
+//     into the caller's arrays (with the x, y, t, p echo) as each DMA lands.
+// Only the last super-chunk's download and copy-out are not hidden by compute.
 extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
@@ -2572,27 +2674,111 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     HIPCHK(hipSetDevice(h->prm.device));
     int rc = ensure_capacity(h, n);
     if (rc) return rc;
+    if ((rc = ensure_pinned(h, n))) return rc;
+    if (!h->s_copy) HIPCHK(hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking));
     hipStream_t s = h->stream;
-    HIPCHK(hipMemcpyAsync(h->x, x, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->y, y, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->t, t, sizeof(uint32_t) * n, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->p, p, sizeof(int32_t) * n, hipMemcpyHostToDevice, s));
+    const int T = host_threads();
+
+    // ---- upload: pinned layout x | y | t | p, n entries each
+    int32_t *px = reinterpret_cast<int32_t *>(h->pin_in), *py = px + n, *pp = py + n;
+    uint32_t *pt = reinterpret_cast<uint32_t *>(pp + n);
+    {
+        std::vector<std::thread> th;
+        std::atomic<int> bad{0};
+        const int64_t slice = std::max<int64_t>((n + T - 1) / T, 1 << 16);
+        for (int64_t a = 0; a < n; a += slice) {
+            const int64_t b = std::min(n, a + slice);
+            auto job = [=, &bad]() {
+                const size_t k = (size_t)(b - a);
+                std::memcpy(px + a, x + a, 4 * k);
+                std::memcpy(py + a, y + a, 4 * k);
+                std::memcpy(pt + a, t + a, 4 * k);
+                std::memcpy(pp + a, p + a, 4 * k);
+                if (hipMemcpyAsync(h->x + a, px + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipMemcpyAsync(h->y + a, py + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipMemcpyAsync(h->t + a, pt + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipMemcpyAsync(h->p + a, pp + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess)
+                    bad = 1;
+            };
+            if (b == n && th.empty()) job();  // one slice: no thread
+            else th.emplace_back(job);
+        }
+        for (auto &w : th) w.join();
+        if (bad) return fail(FARMS_EHIP, "farms_process: host-to-device copy");
+    }
+
+    // ---- compute, with the record downloads hooked onto each super-chunk
     farms_records d{};
     d.r_true = h->o_d[0]; d.theta_true = h->o_d[1]; d.vx = h->o_d[2]; d.vy = h->o_d[3];
     d.r_local = h->o_d[4]; d.theta_local = h->o_d[5]; d.scale = h->o_scale;
-    rc = run_core(h, h->x, h->y, h->t, h->p, n, &d);
+    // pinned layout of the records: six double columns, then scale
+    double *pcol[6];
+    for (int k = 0; k < 6; ++k) pcol[k] = reinterpret_cast<double *>(h->pin_out) + (size_t)k * n;
+    int32_t *pscale = reinterpret_cast<int32_t *>(reinterpret_cast<double *>(h->pin_out) + 6 * (size_t)n);
+    double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
+    double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
+
+    struct Ready { int S, p0, p1; };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Ready> ready;
+    size_t taken = 0;
+    bool closed = false;
+    std::atomic<int> bad{0};
+    auto worker = [&]() {
+        for (;;) {
+            Ready r;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return taken < ready.size() || closed; });
+                if (taken >= ready.size()) return;
+                r = ready[taken++];
+            }
+            if (hipEventSynchronize(h->copy_ev[r.S]) != hipSuccess) { bad = 1; continue; }
+            const size_t k = (size_t)(r.p1 - r.p0);
+            for (int c = 0; c < 6; ++c) std::memcpy(ucol[c] + r.p0, pcol[c] + r.p0, 8 * k);
+            std::memcpy(out->scale + r.p0, pscale + r.p0, 4 * k);
+            // x, y, t, p columns echo the inputs (vFlow.cpp:370-373)
+            std::memcpy(out->x + r.p0, x + r.p0, 4 * k);
+            std::memcpy(out->y + r.p0, y + r.p0, 4 * k);
+            std::memcpy(out->t + r.p0, t + r.p0, 4 * k);
+            std::memcpy(out->p + r.p0, p + r.p0, 4 * k);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 0; i < T; ++i) pool.emplace_back(worker);
+    auto finish = [&](int code) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            closed = true;
+        }
+        cv.notify_all();
+        for (auto &w : pool) w.join();
+        return code;
+    };
+    super_hook hook = [&](int S, int p0, int p1, hipEvent_t done) -> int {
+        while ((int)h->copy_ev.size() <= S) {
+            hipEvent_t ev;
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            h->copy_ev.push_back(ev);
+        }
+        HIPCHK(hipStreamWaitEvent(h->s_copy, done, 0));
+        const size_t k = (size_t)(p1 - p0);
+        for (int c = 0; c < 6; ++c)
+            HIPCHK(hipMemcpyAsync(pcol[c] + p0, dcol[c] + p0, 8 * k, hipMemcpyDeviceToHost, h->s_copy));
+        HIPCHK(hipMemcpyAsync(pscale + p0, d.scale + p0, 4 * k, hipMemcpyDeviceToHost, h->s_copy));
+        HIPCHK(hipEventRecord(h->copy_ev[S], h->s_copy));
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ready.push_back(Ready{S, p0, p1});
+        }
+        cv.notify_one();
+        return FARMS_OK;
+    };
+    rc = run_core(h, h->x, h->y, h->t, h->p, n, &d, &hook);
+    rc = finish(rc);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(out->r_true, d.r_true, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->theta_true, d.theta_true, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->vx, d.vx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->vy, d.vy, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->r_local, d.r_local, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->theta_local, d.theta_local, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(out->scale, d.scale, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    // x, y, t, p columns echo the inputs (vFlow.cpp:370-373)
-    for (int64_t e = 0; e < n; ++e) {
-        out->x[e] = x[e]; out->y[e] = y[e]; out->t[e] = (int32_t)t[e]; out->p[e] = p[e];
-    }
+    if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
+    HIPCHK(hipStreamSynchronize(h->s_copy));
     return FARMS_OK;
 }

@@ -190,8 +190,10 @@ extern "C" int farms_synth_preset(int config, farms_synth_params *o) {
     }
 }
 
-extern "C" int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x, int32_t *y,
-                                        uint32_t *t, int32_t *pol) {
+namespace {
+
+// The whole stream as sorted keys (at least n_events of them), or a negative code.
+int64_t generate_keys(const farms_synth_params *p, std::vector<uint64_t> &keys) {
     if (!p || p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 32767 ||
         p->n_events < 0 || p->n_bars < 0 || p->noise_frac < 0 || p->noise_frac >= 1)
         return -1;
@@ -221,7 +223,7 @@ extern "C" int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x,
     }
     const int64_t n_noise = (int64_t)std::llround((double)p->n_events * p->noise_frac);
     const int64_t n_signal = p->n_events - n_noise;
-    std::vector<uint64_t> keys;
+    keys.clear();
     keys.reserve((size_t)(p->n_events + p->n_events / 16 + 4096));
     // simulate until the signal budget (plus a margin for the tail cut) is reached
     const int64_t margin = n_signal / 64 + 1024;
@@ -249,14 +251,49 @@ extern "C" int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x,
     }
     radix_sort_u64(keys);
     if ((int64_t)keys.size() < p->n_events) return -3;
-    for (int64_t e = 0; e < p->n_events; ++e) {
-        const uint64_t k = keys[(size_t)e];
-        t[e] = (uint32_t)(k >> 32);
-        x[e] = (int32_t)((k >> 16) & 0xFFFF);
-        y[e] = (int32_t)((k >> 1) & 0x7FFF);
-        pol[e] = (k & 1) ? 1 : -1;
-    }
     return p->n_events;
+}
+
+inline void unpack(uint64_t k, int32_t &x, int32_t &y, uint32_t &t, int32_t &pol) {
+    t = (uint32_t)(k >> 32);
+    x = (int32_t)((k >> 16) & 0xFFFF);
+    y = (int32_t)((k >> 1) & 0x7FFF);
+    pol = (k & 1) ? 1 : -1;
+}
+
+}  // namespace
+
+extern "C" int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x, int32_t *y,
+                                        uint32_t *t, int32_t *pol) {
+    std::vector<uint64_t> keys;
+    const int64_t n = generate_keys(p, keys);
+    if (n <= 0) return n;
+    for (int64_t e = 0; e < n; ++e) unpack(keys[(size_t)e], x[e], y[e], t[e], pol[e]);
+    return n;
+}
+
+extern "C" int64_t farms_synth_generate_select(const farms_synth_params *p, int64_t e0, int64_t e1,
+                                               int32_t x_lo, int32_t x_hi, int64_t cap, int32_t *x,
+                                               int32_t *y, uint32_t *t, int32_t *pol, int64_t *idx,
+                                               uint32_t *t_first) {
+    if (!p || e0 < 0 || e1 < e0 || cap < 0 || (cap > 0 && (!x || !y || !t || !pol))) return -1;
+    std::vector<uint64_t> keys;
+    const int64_t n = generate_keys(p, keys);
+    if (n < 0) return n;
+    if (t_first) *t_first = n > 0 ? (uint32_t)(keys[0] >> 32) : 0u;
+    if (e1 > n) e1 = n;
+    int64_t m = 0;
+    for (int64_t e = e0; e < e1; ++e) {
+        const uint64_t k = keys[(size_t)e];
+        const int32_t kx = (int32_t)((k >> 16) & 0xFFFF);
+        if (kx < x_lo || kx >= x_hi) continue;
+        if (m < cap) {
+            unpack(k, x[m], y[m], t[m], pol[m]);
+            if (idx) idx[m] = e;
+        }
+        ++m;
+    }
+    return m;
 }
 
 extern "C" int farms_synth_write_text(const char *path, const int32_t *x, const int32_t *y,
@@ -271,4 +308,14 @@ extern "C" int farms_synth_write_text(const char *path, const int32_t *x, const 
     }
     std::fwrite(buf.data(), 1, used, f);
     return std::fclose(f) == 0 ? 0 : -1;
+}
+
+extern "C" int farms_synth_column_hist(const farms_synth_params *p, int64_t *hist) {
+    if (!p || !hist) return -1;
+    std::vector<uint64_t> keys;
+    const int64_t n = generate_keys(p, keys);
+    if (n < 0) return (int)n;
+    std::memset(hist, 0, sizeof(int64_t) * (size_t)p->width);
+    for (int64_t e = 0; e < n; ++e) hist[(keys[(size_t)e] >> 16) & 0xFFFF]++;
+    return 0;
 }

@@ -55,6 +55,7 @@ class FarmsParams(ctypes.Structure):
         ("own_x0", ctypes.c_int32),
         ("own_x1", ctypes.c_int32),
         ("pool_batch", ctypes.c_int32),
+        ("serial", ctypes.c_int32),
     ]
 
 
@@ -109,9 +110,10 @@ HIP_SYMBOLS = (
     "farms_default_params", "farms_create", "farms_destroy", "farms_reset", "farms_process",
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
     "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
-    "farms_seed_sae",
+    "farms_seed_sae", "farms_serial_first",
 )
-SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text")
+SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text",
+                 "farms_synth_generate_select", "farms_synth_column_hist")
 
 _hip = None
 _synth = None
@@ -163,6 +165,10 @@ def load_synth_library() -> ctypes.CDLL:
     lib.farms_synth_generate.restype = ctypes.c_int64
     lib.farms_synth_generate.argtypes = [ctypes.c_void_p] * 5
     lib.farms_synth_write_text.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64]
+    lib.farms_synth_generate_select.restype = ctypes.c_int64
+    lib.farms_synth_generate_select.argtypes = ([ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                                 ctypes.c_int32, ctypes.c_int64] + [ctypes.c_void_p] * 6)
+    lib.farms_synth_column_hist.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     _synth = lib
     return lib
 
@@ -191,10 +197,14 @@ class Events:
     def head(self, n: int) -> "Events":
         return Events(self.x[:n].copy(), self.y[:n].copy(), self.t[:n].copy(), self.p[:n].copy())
 
-    def relative(self) -> tuple:
+    def relative(self, t0: int | None = None) -> tuple:
         """Host prologue of runFileCopy: t - t0 as uint32 (vFlow.cpp:194, 240-241)
-        and polarity clamped to >= 0 (vFlow.cpp:245-247)."""
-        t0 = np.uint32(self.t[0]) if len(self) else np.uint32(0)
+        and polarity clamped to >= 0 (vFlow.cpp:245-247).  t0 defaults to the
+        first stamp; a share of a longer stream passes the stream's."""
+        if t0 is not None:
+            t0 = np.uint32(t0)
+        else:
+            t0 = np.uint32(self.t[0]) if len(self) else np.uint32(0)
         t_rel = (self.t.astype(np.uint32) - t0).astype(np.uint32)
         p = np.maximum(self.p, 0).astype(np.int32)
         return (np.ascontiguousarray(self.x, dtype=np.int32), np.ascontiguousarray(self.y, dtype=np.int32),
@@ -256,6 +266,37 @@ def synth_generate(params: SynthParams) -> Events:
     return Events(x, y, t, p)
 
 
+def synth_select(params: SynthParams, e0: int, e1: int, x_lo: int = 0, x_hi: int | None = None):
+    """Events [e0, e1) of the stream with column in [x_lo, x_hi), their stream
+    indices and the stream's first stamp, without materialising the whole
+    stream (farms_synth_generate_select): one rank's share."""
+    lib = load_synth_library()
+    x_hi = int(params.width) if x_hi is None else int(x_hi)
+    e1 = min(int(e1), int(params.n_events))
+    cap = max(e1 - int(e0), 0)
+    x = np.empty(cap, np.int32)
+    y = np.empty(cap, np.int32)
+    t = np.empty(cap, np.uint32)
+    p = np.empty(cap, np.int32)
+    idx = np.empty(cap, np.int64)
+    t_first = ctypes.c_uint32(0)
+    got = lib.farms_synth_generate_select(ctypes.byref(params), ctypes.c_int64(int(e0)), ctypes.c_int64(e1),
+                                          ctypes.c_int32(int(x_lo)), ctypes.c_int32(x_hi), ctypes.c_int64(cap),
+                                          _ptr(x), _ptr(y), _ptr(t), _ptr(p), _ptr(idx), ctypes.byref(t_first))
+    if got < 0 or got > cap:
+        raise RuntimeError(f"farms_synth_generate_select returned {got}")
+    return Events(x[:got].copy(), y[:got].copy(), t[:got].copy(), p[:got].copy()), idx[:got].copy(), int(t_first.value)
+
+
+def synth_column_hist(params: SynthParams) -> np.ndarray:
+    """Events per column of the whole stream (farms_synth_column_hist)."""
+    lib = load_synth_library()
+    hist = np.zeros(int(params.width), np.int64)
+    if lib.farms_synth_column_hist(ctypes.byref(params), _ptr(hist)) != 0:
+        raise RuntimeError("farms_synth_column_hist failed")
+    return hist
+
+
 def synth_config(config: int, n_events: int | None = None) -> Events:
     return synth_generate(synth_params(config, n_events))
 
@@ -285,7 +326,7 @@ class FlowManager:
     def __init__(self, height: int = 320, width: int = 320, filter_size: int = 3, min_evts_on_plane: int = 5,
                  window_jump: int = 5, max_window: int = 50, device: int = 0, fit_chunk: int = 0,
                  pool_chunk: int = 0, region: tuple | None = None, owned: tuple | None = None,
-                 pool_batch: int = 0):
+                 pool_batch: int = 0, serial: bool = False):
         self._lib = load_hip_library()
         prm = FarmsParams()
         _check(self._lib, self._lib.farms_default_params(ctypes.byref(prm)))
@@ -294,6 +335,7 @@ class FlowManager:
         prm.window_jump, prm.max_window = int(window_jump), int(max_window)
         prm.device, prm.fit_chunk, prm.pool_chunk = int(device), int(fit_chunk), int(pool_chunk)
         prm.pool_batch = int(pool_batch)
+        prm.serial = 1 if serial else 0
         if region is not None:  # (x0, x1): stored columns
             prm.region_x0, prm.region_width = int(region[0]), int(region[1]) - int(region[0])
         if owned is not None:  # (x0, x1): pooled columns
@@ -336,7 +378,9 @@ class FlowManager:
         _check(self._lib, self._lib.farms_get_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
 
-    def process(self, x, y, t_rel, p) -> Records:
+    def process(self, x, y, t_rel, p, out: Records | None = None) -> Records:
+        """farms_process: host arrays in, host records out (into `out` when
+        given, e.g. to reuse its pages across calls)."""
         x = np.ascontiguousarray(x, dtype=np.int32)
         y = np.ascontiguousarray(y, dtype=np.int32)
         t_rel = np.ascontiguousarray(t_rel, dtype=np.uint32)
@@ -344,11 +388,19 @@ class FlowManager:
         n = int(x.shape[0])
         if not (y.shape[0] == t_rel.shape[0] == p.shape[0] == n):
             raise ValueError("x, y, t, p must have the same length")
-        rec = Records(n)
-        out = rec.as_c()
+        rec = Records(n) if out is None else out
+        if rec.n != n:
+            raise ValueError("records length differs from the event count")
+        oc = rec.as_c()
         _check(self._lib, self._lib.farms_process(self._h, _ptr(x), _ptr(y), _ptr(t_rel), _ptr(p), n,
-                                                  ctypes.byref(out)))
+                                                  ctypes.byref(oc)))
         return rec
+
+    def serial_first(self, x: int, y: int, t_abs: int) -> None:
+        """Serial mode: the file's first line only stamps lastEventTime
+        (vFlow.cpp:531-556); call before the first process()."""
+        _check(self._lib, self._lib.farms_serial_first(self._h, ctypes.c_int32(int(x)), ctypes.c_int32(int(y)),
+                                                       ctypes.c_uint32(int(t_abs) & 0xFFFFFFFF)))
 
     def process_events(self, ev: Events) -> Records:
         return self.process(*ev.relative())

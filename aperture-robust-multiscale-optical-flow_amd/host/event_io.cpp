@@ -181,9 +181,15 @@ int64_t parse_events(const char *text, size_t len, uint64_t max_events, EventCol
 
 bool read_events(const std::string &path, uint64_t max_events, EventColumns &cols, int64_t &n_read) {
     n_read = 0;
+    std::string text;
+    if (!read_text(path, text)) return false;
+    n_read = parse_events(text.data(), text.size(), max_events, cols);
+    return true;
+}
+
+bool read_text(const std::string &path, std::string &text) {
     FILE *f = fopen(path.c_str(), "rb");
     if (!f) return false;
-    std::string text;
     char buf[1 << 16];
     if (fseek(f, 0, SEEK_END) == 0) {
         const long sz = ftell(f);
@@ -193,8 +199,50 @@ bool read_events(const std::string &path, uint64_t max_events, EventColumns &col
     size_t got;
     while ((got = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, got);
     fclose(f);
-    n_read = parse_events(text.data(), text.size(), max_events, cols);
     return true;
+}
+
+int64_t parse_events_serial(const char *text, size_t len, uint64_t numevents, SerialEvents &out) {
+    const char *p = text, *const end = text + len;
+    int x = 0, y = 0, pol = 0;  // vFlow.cpp:494 (uninitialised there)
+    unsigned int time_ = 0;
+    auto line = [&](const char *&b, const char *&e) -> bool {  // getline
+        if (p >= end) return false;
+        const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+        b = p;
+        e = nl ? nl : end;
+        p = nl ? nl + 1 : end;
+        return true;
+    };
+    const char *b, *e;
+    out.has_first = false;
+    if (!line(b, e)) return 0;
+    {  // the first line: only lastEventTime[x][y] = time_, t0 = time_ (vFlow.cpp:531-556)
+        bool fail = false;
+        extract(b, e, x, fail);
+        extract(b, e, y, fail);
+        extract(b, e, time_, fail);
+        extract(b, e, pol, fail);
+        out.has_first = true;
+        out.x0 = x; out.y0 = y; out.t0 = time_;
+    }
+    const unsigned int t0 = time_;
+    uint64_t computed = 0;  // eventsComputed (vFlow.cpp:76)
+    while (line(b, e) && computed <= numevents) {  // vFlow.cpp:565
+        bool fail = false;
+        extract(b, e, x, fail);
+        extract(b, e, y, fail);
+        extract(b, e, time_, fail);
+        time_ = time_ - t0;  // applied to a carried value too (vFlow.cpp:573)
+        extract(b, e, pol, fail);
+        if (pol < 0) pol = 0;  // vFlow.cpp:577-578
+        out.cols.X.push_back(x);
+        out.cols.Y.push_back(y);
+        out.cols.T.push_back(time_);
+        out.cols.POL.push_back(pol);
+        ++computed;
+    }
+    return (int64_t)computed;
 }
 
 static size_t put_record(char *dst, const farms_records &r, int64_t i) {
@@ -284,4 +332,17 @@ extern "C" int64_t farms_io_format(const farms_records *r, int64_t n, char *out,
 
 extern "C" int farms_io_write(const char *path, const farms_records *r, int64_t n) {
     return farms_io::write_records(path, *r, n) ? 0 : -1;
+}
+
+extern "C" int64_t farms_io_parse_serial(const char *text, int64_t len, int64_t numevents, int32_t *first3,
+                                         int32_t *x, int32_t *y, uint32_t *t, int32_t *p, int64_t cap) {
+    farms_io::SerialEvents se;
+    const int64_t n = farms_io::parse_events_serial(text, (size_t)len, (uint64_t)numevents, se);
+    if (n > cap) return -1;
+    first3[0] = se.has_first ? 1 : 0;
+    first3[1] = se.x0; first3[2] = se.y0; first3[3] = (int32_t)se.t0;
+    for (int64_t i = 0; i < n; ++i) {
+        x[i] = se.cols.X[(size_t)i]; y[i] = se.cols.Y[(size_t)i]; t[i] = se.cols.T[(size_t)i]; p[i] = se.cols.POL[(size_t)i];
+    }
+    return n;
 }

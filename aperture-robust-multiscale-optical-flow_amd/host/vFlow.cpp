@@ -6,6 +6,7 @@
 // The per-event loop (vFlow.cpp:223-414) is one farms_process call.
 #include "vFlow.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <iostream>
@@ -65,6 +66,10 @@ long vFlowManager::process(bool write_output) {
     const unsigned int t0 = T.at(0);
     std::cout << "First time = " << t0 << std::endl;
     std::cout << "Processing events " << std::endl;
+    if (prm.serial) {  // runFileCopy after run(): batch semantics again
+        prm.serial = 0;
+        close();
+    }
     int rc = ensure_handle();
     if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_create: ") + farms_last_error());
 
@@ -110,22 +115,53 @@ long vFlowManager::runFileCopy(unsigned long int NUMEVENTS) {
     return process(true);
 }
 
-// Serial mode (vFlow.cpp:465-826) is the reference's streaming variant: it
-// writes no output file and reports the summed per-event compute time.  Here it
-// runs the same accelerated loop and reports its time; its per-event semantics
-// (first event skipped, lastEventTime written after pooling) are not
-// reproduced — see DESIGN.md §7.
+// Serial mode (vFlow.cpp:465-826), the reference CLI's default: the first
+// line only stamps lastEventTime (farms_serial_first), the loop runs over at
+// most NUMEVENTS + 1 further lines with the engine's serial semantics
+// (lastEventTime written after pooling, farms_params.serial) and writes no
+// output; returns the microseconds of the accelerated loop.  The reference's
+// per-event "Local ..." / "true ..." timing lines (vFlow.cpp:626, 733) are not
+// printed: the loop is one batched call.
 long vFlowManager::run(unsigned long int NUMEVENTS) {
-    const std::string in = fileNameInput + ".txt";
+    const std::string in = fileNameInput + ".txt";  // vFlow.cpp:497
     std::cout << in << std::endl;
-    farms_io::EventColumns cols;
-    int64_t nread = 0;
-    if (!farms_io::read_events(in, NUMEVENTS, cols, nread)) {
+    std::string text;
+    if (!farms_io::read_text(in, text)) {
         std::cout << "Unable to open file" << std::endl;  // vFlow.cpp:802
+        std::cout << std::endl << "Done!" << std::endl;
         return 0;
     }
-    X = cols.X; Y = cols.Y; T = cols.T; POL = cols.POL;
-    const long us = process(false);
-    std::cout << std::endl << "Done!" << std::endl;
+    // NUMEVENTS = min(NUMEVENTS, fsize / 18) (vFlow.cpp:513)
+    NUMEVENTS = (unsigned long int)std::min<double>((double)NUMEVENTS, (double)(text.size() / 18));
+    farms_io::SerialEvents se;
+    const int64_t n = farms_io::parse_events_serial(text.data(), text.size(), NUMEVENTS, se);
+    std::string().swap(text);
+    if (!se.has_first) {
+        std::cout << std::endl << "Done!" << std::endl;
+        return 0;
+    }
+    std::cout << "First time = " << se.t0 << std::endl;  // vFlow.cpp:549
+    if (!prm.serial) {
+        prm.serial = 1;
+        close();
+    }
+    int rc = ensure_handle();
+    if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_create: ") + farms_last_error());
+    rc = farms_serial_first(handle, se.x0, se.y0, se.t0);
+    if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_serial_first: ") + farms_last_error());
+    long us = 0;
+    if (n > 0) {
+        std::vector<int32_t> ox((size_t)n), oy((size_t)n), ot((size_t)n), op((size_t)n), osc((size_t)n);
+        std::vector<double> rt((size_t)n), tt((size_t)n), vx((size_t)n), vy((size_t)n), rl((size_t)n), tl((size_t)n);
+        farms_records rec{ox.data(), oy.data(), ot.data(), op.data(), rt.data(), tt.data(),
+                          vx.data(), vy.data(), rl.data(), tl.data(), osc.data()};
+        const auto start = std::chrono::system_clock::now();
+        rc = farms_process(handle, se.cols.X.data(), se.cols.Y.data(), se.cols.T.data(), se.cols.POL.data(), n, &rec);
+        const auto stop = std::chrono::system_clock::now();
+        if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_process: ") + farms_last_error());
+        us = (long)std::chrono::duration_cast<std::chrono::microseconds>(stop - start).count();
+        numEvents += (double)n;  // this->numEvents = eventsComputed (vFlow.cpp:792)
+    }
+    std::cout << std::endl << "Done!" << std::endl;  // vFlow.cpp:808
     return us;
 }

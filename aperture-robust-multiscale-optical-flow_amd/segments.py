@@ -65,19 +65,61 @@ def plan(t_rel: np.ndarray, n_seg: int) -> list[Segment]:
         raise ValueError("need 1 <= segments <= events")
     if not is_time_ordered(t):
         raise ValueError("temporal segments need non-decreasing stamps; use strips.plan")
-    cuts = [r * n // n_seg for r in range(n_seg + 1)]
+    cut = cuts(n, n_seg)
     segs = []
     for r in range(n_seg):
-        start, end = cuts[r], cuts[r + 1]
+        start, end = cut[r], cut[r + 1]
         warm = start
         if r > 0 and start < n:
             # every event with t > t[start] - 500 before start (it may still
             # contribute to an owned event)
             warm = int(np.searchsorted(t[:start], t[start] - KILL_US, side="right"))
-            if warm < cuts[r - 1]:
+            if warm < cut[r - 1]:
                 raise ValueError("segment shorter than the 500 us warm-up; use fewer segments")
         segs.append(Segment(r, start, end, warm))
     return segs
+
+
+WARM_MAX = 4_000_000  # bound on a warm-up's length for plan_rank's stream window (events)
+
+
+def cuts(n: int, n_seg: int) -> list[int]:
+    return [r * n // n_seg for r in range(n_seg + 1)]
+
+
+def rank_window(n: int, n_seg: int, r: int, warm_max: int = WARM_MAX) -> tuple[int, int]:
+    """Stream indices [lo, hi) whose stamps plan_rank needs for rank r: its
+    segment, up to warm_max events before it (its warm-up) and the events up to
+    the next cut (the next rank's warm-up, which ends rank r's head)."""
+    c = cuts(n, n_seg)
+    return max(0, c[r] - warm_max), min(n, c[r + 1] + 1)
+
+
+def plan_rank(t_window: np.ndarray, lo: int, n: int, n_seg: int, r: int) -> tuple[Segment, int]:
+    """Segment r and its head length from the stamps of rank_window(n, n_seg, r)
+    only (t_window = t[lo:hi]): what plan() and head_length() give on the whole
+    stream, for ranks that never hold it."""
+    t = np.asarray(t_window).astype(np.int64)
+    if not is_time_ordered(t):
+        raise ValueError("temporal segments need non-decreasing stamps; use strips")
+    c = cuts(n, n_seg)
+    start, end = c[r], c[r + 1]
+
+    def warm_of(k: int) -> int:  # first event with t > t[k] - 500 (k > 0)
+        w = lo + int(np.searchsorted(t[:k - lo], t[k - lo] - KILL_US, side="right"))
+        if w == lo and lo > 0:
+            raise ValueError("warm-up longer than the planning window; raise WARM_MAX")
+        return w
+
+    warm = start
+    if r > 0 and start < n:
+        warm = warm_of(start)
+        if warm < c[r - 1]:
+            raise ValueError("segment shorter than the 500 us warm-up; use fewer segments")
+    head = end - start
+    if r + 1 < n_seg and end < n:
+        head = warm_of(end) - start
+    return Segment(r, start, end, warm), head
 
 
 def head_length(segs: list[Segment], r: int) -> int:

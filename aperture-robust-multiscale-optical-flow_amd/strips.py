@@ -44,10 +44,16 @@ class Strip:
 
 def plan(x: np.ndarray, width: int, n_strips: int, filter_size: int, max_window: int) -> list[Strip]:
     """Column ranges for n_strips ranks, balanced by the events of `x`."""
+    return plan_hist(np.bincount(np.asarray(x, dtype=np.int64), minlength=width), n_strips, filter_size, max_window)
+
+
+def plan_hist(hist: np.ndarray, n_strips: int, filter_size: int, max_window: int) -> list[Strip]:
+    """Column ranges for n_strips ranks, balanced by a per-column event count
+    (farms.synth_column_hist for a synthetic stream no rank holds whole)."""
+    width = int(len(hist))
     if n_strips < 1 or n_strips > width:
         raise ValueError("need 1 <= n_strips <= width")
-    hist = np.bincount(np.asarray(x, dtype=np.int64), minlength=width).astype(np.float64)
-    cum = np.cumsum(hist)
+    cum = np.cumsum(np.asarray(hist, dtype=np.float64))
     total = cum[-1] if cum.size else 0.0
     cuts = [0]
     for r in range(1, n_strips):

@@ -24,6 +24,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,7 +57,28 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", choices=("segments", "strips"), default="segments",
                     help="N > 1: temporal segments (time-ordered streams) or x-strips")
+    ap.add_argument("--host-steps", type=int, default=2,
+                    help="N=1: steps of the host-array path (farms_process: H2D + kernels + D2H) timed after "
+                         "the device-resident ones (0 = skip)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="launch, rendezvous, per-rank stream shares and partition only; no GPU, no timing "
+                         "(CPU test of the multi-rank plumbing; value is null)")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return int(so.getsockname()[1])
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start the N ranks as a
+    child torchrun on this node (one process per GPU), before anything touches
+    the GPU, and return its exit code.  Its rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def cpu_baseline(sample, width, height, fs, jump, maxw):
@@ -99,80 +122,175 @@ def parity_vs_cpu(ref, out, k):
             "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"]}
 
 
-def pmc_traffic(cfg, world, pool_launches):
-    """HBM bytes per k_pool launch from the committed rocprofv3 PMC passes of the
-    same workload (tools/gpu_traffic.sh -> profiles/rNN_traffic_c<cfg>.json,
-    FETCH_SIZE doubled per the gfx950 correction).  None unless the profile saw
-    whole steps of this launch count (i.e. the same stream and chunking)."""
+def committed_profile(kind: str, cfg: int, world: int, pool_launches: int, kernel: str):
+    """Per-kernel figures for the dominant kernel from the newest committed
+    rocprofv3 PMC summary of the same workload (profiles/rNN_<kind>_c<cfg>.json,
+    made by tools/gpu_traffic.sh / tools/gpu_sq.sh from `bench.py --steps 1
+    --warmup 0`).  None unless the profile saw whole steps of this launch count
+    (the same stream and chunking)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_traffic_c{cfg}.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_c{cfg}.json")))
     if world != 1 or not files:
         return None
-    k = json.load(open(files[-1]))["kernels"].get("k_pool<11>" if cfg != 5 else "k_pool<3>")
-    if not k or k["dispatches"] % pool_launches:  # the profiled run made whole steps of this workload
+    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    if not k or k["dispatches"] % pool_launches:
         return None
-    return round(k["traffic_bytes_per_launch"])
+    return dict(k, source=os.path.relpath(files[-1], ROOT))
+
+
+def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense_bytes: float) -> dict:
+    """Roofline of the dominant kernel, k_pool.
+
+    achieved = HBM bytes per launch measured by the PMC counters (2 x
+    FETCH_SIZE + WRITE_SIZE, the gfx950 correction) / the launch's average
+    duration, timed live with HIP events on the pooling stream; frac = achieved
+    / 8 TB/s.  The kernel is not HBM-bound (it reads a chunk's candidate lists
+    from L2): `issue` gives the bound that binds, from the SQ counters of the
+    same workload (VALU issue utilisation, waits).  SURVEY §8d's dense-window
+    figure (20 B per window cell of a valid event) is reported apart as
+    dense_equiv_*: the kernel never reads the dense window, so that figure
+    divided by the time exceeds HBM peak and is no physical rate."""
+    kname = "k_pool<11>" if cfg != 5 else "k_pool<3>"
+    tr = committed_profile("traffic", cfg, world, pool_launches, kname)
+    sq = committed_profile("sq", cfg, world, pool_launches, kname)
+    traffic = round(tr["traffic_bytes_per_launch"]) if tr else None
+    achieved = traffic / (avg_us * 1e-6) / 1e9 if traffic and avg_us > 0 else None
+    dense_per_launch = dense_bytes / max(pool_launches, 1)
+    r = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+         "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
+         "traffic_source": tr["source"] if tr else None,
+         "kernel": "k_pool", "launches_per_step": pool_launches, "avg_launch_us": round(avg_us, 2),
+         "dense_equiv_bytes_per_launch": round(dense_per_launch),
+         "dense_equiv_GBps": round(dense_per_launch / (avg_us * 1e-6) / 1e9, 1) if avg_us > 0 else None}
+    if sq:
+        waves = max(sq["SQ_WAVES"], 1.0)
+        wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
+        # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; a wave64
+        # VALU instruction issues over 4 of them
+        simd_cycles = 1024 * 2.4e9 * avg_us * 1e-6
+        r["issue"] = {"valu_insts_per_wave": round(sq["SQ_INSTS_VALU"] / waves, 1),
+                      "valu_issue_util": round(4.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
+                      "wait_any_frac": round(sq["SQ_WAIT_ANY"] / wave_cyc, 4),
+                      "wait_inst_frac": round(sq["SQ_WAIT_INST_ANY"] / wave_cyc, 4),
+                      "active_inst_frac": round(sq["SQ_ACTIVE_INST_ANY"] / wave_cyc, 4),
+                      "source": sq["source"]}
+    return r
+
+
+def host_path(fm, x, y, t, p, steps: int) -> dict:
+    """The boundary as the CLI uses it (vFlow.cpp:214-416): host arrays in,
+    host records out through farms_process — pinned staging, H2D, the kernels,
+    overlapped D2H of finished pooling super-chunks, copy-out and the x/y/t/p
+    echo.  Timed apart from `value`, which keeps inputs resident in HBM."""
+    rec = farms.Records(len(x))
+    fm.set_profiling(0)
+    fm.reset()
+    fm.process(x, y, t, p, out=rec)  # warm-up: pinned staging, output pages
+    best, tot = 1e30, 0.0
+    for _ in range(steps):
+        fm.reset()
+        t0 = time.perf_counter()
+        fm.process(x, y, t, p, out=rec)
+        dt = time.perf_counter() - t0
+        best, tot = min(best, dt), tot + dt
+    return {"value": round(len(x) * steps / tot / 1e6, 3), "unit": "Mevents/s", "steps": steps,
+            "ms_per_step": round(tot / steps * 1e3, 3), "ms_best": round(best * 1e3, 3),
+            "what": "farms_process host-to-host: pinned staging + H2D of 16 B/event, kernels, D2H of 52 B/event "
+                    "overlapped per pooling super-chunk, copy-out and x/y/t/p echo (FARMS_HOST_THREADS threads)"}
+
+
+def rank_share(args, cfg: int, world: int, rank: int) -> dict:
+    """This rank's events of the weak-scaling stream (world x per-GPU events on
+    one sensor), generated without materialising the whole stream on any rank
+    (farms.synth_select): relative stamps (the stream's t0), clamped polarity."""
+    W, H = SENSOR[cfg]
+    fs = FILTER[cfg]
+    maxw = 50
+    sp = farms.synth_params(cfg)
+    per_gpu = args.events or (int(sp.n_events) if cfg in (1, 2, 3) else 50_000_000)
+    n = per_gpu * world
+    sp.n_events = n
+    sh = {"per_gpu": per_gpu, "n_stream": n, "region": None, "owned": None, "seg": None, "cpu_sample": None}
+    if world == 1:
+        ev = farms.synth_generate(sp)
+        sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative()
+        if not args.no_cpu_baseline and not args.plan_only:
+            sh["cpu_sample"] = ev.head(min(args.cpu_sample, len(ev)))
+        sh.update(split="none", n_owned=n, label="1 GPU")
+    elif args.split == "segments":
+        lo, hi = segments.rank_window(n, world, rank)
+        ev, _, t_first = farms.synth_select(sp, lo, hi)
+        x, y, t, p = ev.relative(t_first)
+        seg, n_head = segments.plan_rank(t, lo, n, world, rank)  # raises on an unordered stream
+        sl = slice(seg.warm - lo, seg.end - lo)
+        sh["x"], sh["y"], sh["t"], sh["p"] = x[sl], y[sl], t[sl], p[sl]
+        sh.update(split="segments", seg=seg, n_head=n_head, n_owned=seg.end - seg.start,
+                  label=(f"{world} temporal segments of the time-ordered stream: per step the ranks' last-stamp "
+                         f"surfaces are all-gathered and each rank starts from the merged SAE plus a re-fitted "
+                         f"500 us warm-up ({seg.n_warm} events on rank {rank})"))
+    else:
+        strip = strips.plan_hist(farms.synth_column_hist(sp), world, fs, maxw)[rank]
+        ev, _, t_first = farms.synth_select(sp, 0, n, strip.reg_lo, strip.reg_hi)
+        sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative(t_first)
+        sh.update(split="strips", region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi),
+                  n_owned=int(strips.owned_mask(sh["x"], strip).sum()),
+                  label=f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, no data-path collective")
+    return sh
 
 
 def main():
     args = parse()
-    import torch
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    import torch
+
     # FARMS_BENCH_DEVICE pins every rank to one device (rehearsal of N ranks on a
     # one-GPU box, with FARMS_DIST_BACKEND=gloo); the driver uses neither.
     device = int(os.environ.get("FARMS_BENCH_DEVICE", local_rank))
-    backend = os.environ.get("FARMS_DIST_BACKEND", "nccl")
+    backend = os.environ.get("FARMS_DIST_BACKEND", "gloo" if args.plan_only else "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(device)
+        if not args.plan_only:
+            torch.cuda.set_device(device)
         dist.init_process_group(backend)
-    dev = torch.device("cuda", device)
-    red_dev = dev if backend == "nccl" else torch.device("cpu")
+    red_dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
 
     cfg = args.config
     W, H = SENSOR[cfg]
     fs = FILTER[cfg]
     jump, maxw = (25, 50) if cfg == 5 else (5, 50)
-    sp = farms.synth_params(cfg)
-    per_gpu = args.events or (int(sp.n_events) if cfg in (1, 2, 3) else 50_000_000)
-    sp.n_events = per_gpu * world  # weak scaling: fixed events per GPU
-    ev = farms.synth_generate(sp)  # same seed on every rank: the same stream
-    x, y, t, p = ev.relative()
-    cpu_sample = ev.head(min(args.cpu_sample, len(ev))) if world == 1 and not args.no_cpu_baseline else None
-    del ev
-    # N > 1: temporal segments on a time-ordered stream (DESIGN.md §6), x-strips
-    # otherwise (or with --split strips)
-    split = "none" if world == 1 else args.split
-    if split == "segments" and not segments.is_time_ordered(t):
-        split = "strips"
-    region, owned, seg = None, None, None
-    if split == "segments":
-        segs = segments.plan(t, world)
-        seg = segs[rank]
-        n_head = segments.head_length(segs, rank)
-        sl = slice(seg.warm, seg.end)
-        x, y, t, p = x[sl], y[sl], t[sl], p[sl]
-        n_owned = seg.end - seg.start
-        label = (f"{world} temporal segments of the time-ordered stream: per step the ranks' last-stamp "
-                 f"surfaces are all-gathered over {backend.upper()} and each rank starts from the merged SAE "
-                 f"plus a re-fitted 500 us warm-up ({seg.n_warm} events on rank {rank})")
-    elif split == "strips":
-        strip = strips.plan(x, W, world, fs, maxw)[rank]
-        m = strips.region_mask(x, strip)
-        x, y, t, p = x[m], y[m], t[m], p[m]
-        region, owned = (strip.reg_lo, strip.reg_hi), (strip.own_lo, strip.own_hi)
-        n_owned = int(strips.owned_mask(x, strip).sum())
-        label = f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, no data-path collective"
-    else:
-        n_owned = len(x)
-        label = "1 GPU"
+    sh = rank_share(args, cfg, world, rank)
+    x, y, t, p = sh["x"], sh["y"], sh["t"], sh["p"]
+    per_gpu, n_owned, split, seg, label = sh["per_gpu"], sh["n_owned"], sh["split"], sh["seg"], sh["label"]
+    cpu_sample = sh["cpu_sample"]
     n = len(x)
+    if args.plan_only:
+        total = n_owned
+        if dist:
+            tt = torch.tensor([n_owned], dtype=torch.int64)
+            dist.all_reduce(tt)
+            total = int(tt.item())
+        line = {"metric": "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref",
+                "value": None, "unit": "Mevents/s", "n_gpus": world, "plan_only": True,
+                "config": {"workload": f"BASELINE config {cfg}", "events_per_gpu": per_gpu, "parallelism": label},
+                "detail": {"owned_events_all_ranks": total, "stream_events": sh["n_stream"],
+                           "rank0_stored_events": n, "rank0_owned_events": n_owned}}
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+    dev = torch.device("cuda", device)
     dx = torch.from_numpy(x).to(dev)
     dy = torch.from_numpy(y).to(dev)
     dt_ = torch.from_numpy(t.view(np.int32)).to(dev)
@@ -180,8 +298,9 @@ def main():
     out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
            for c in farms.COLUMNS[4:]}
     fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=region, owned=owned)
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=sh["region"], owned=sh["owned"])
     if seg is not None:  # stamp surfaces: this rank's [head, full], everyone's, the merged SAE
+        n_head = sh["n_head"]
         WHs = W * H
         mine = torch.empty((2, WHs), dtype=torch.int64, device=dev)
         gath = torch.empty((2 * world, WHs), dtype=torch.int64, device=red_dev)
@@ -239,14 +358,9 @@ def main():
     fm.set_profiling(True)
     step()
     st = fm.stats()
-    alg_bytes = 20.0 * st["pool_cells"]  # 20 B per pooled cell of a valid event
-    achieved = alg_bytes / (pool_ms / 1e3) / 1e9 if pool_ms > 0 else 0.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(cfg, world, pool_launches),
-                "traffic_unit": "HBM bytes per launch (PMC)",
-                "algorithmic_bytes_per_launch": round(alg_bytes / max(pool_launches, 1)),
-                "kernel": "k_pool", "launches_per_step": pool_launches,
-                "avg_launch_us": round(pool_ms * 1e3 / max(pool_launches, 1), 2)}
+    avg_us = pool_ms * 1e3 / max(pool_launches, 1)
+    dense_bytes = 20.0 * st["pool_cells"]  # 20 B per dense pooling-window cell of a valid event
+    roofline = pool_roofline(cfg, world, pool_launches, avg_us, dense_bytes)
     line = {
         "metric": "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref",
         "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
@@ -261,10 +375,12 @@ def main():
                    "ms_prep": round(ts["ms_prep"], 3), "ms_fit_sweep": round(ts["ms_fit"], 3),
                    "ms_pool_sweep": round(ts["ms_pool"], 3), "ms_pool_kernel": round(pool_ms, 3),
                    "ms_fit_kernel_untimed_step": round(st["ms_fit_kernel"], 3),
-                   "dense_equiv_bytes_per_event": round(alg_bytes / max(n, 1), 1),
+                   "dense_equiv_bytes_per_event": round(dense_bytes / max(n, 1), 1),
                    "cand_per_valid": round(st["pool_candidates"] / max(st["n_valid"], 1), 1),
                    "contrib_per_valid": round(st["pool_contributors"] / max(st["n_valid"], 1), 1)},
     }
+    if world == 1 and args.host_steps > 0:
+        line["host_path"] = host_path(fm, x, y, t, p, args.host_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ref, line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
         line["parity"] = parity_vs_cpu(ref, out, len(cpu_sample))

@@ -57,6 +57,12 @@ typedef struct {
     int32_t region_x0, region_width;
     int32_t own_x0, own_x1;
     int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64; 32 at filtersize 7) */
+    /* 1: the per-event semantics of vFlowManager::run (vFlow.cpp:465-826, the
+     * CLI's --SERIAL 1, its default): lastEventTime is written after pooling
+     * (:790), so an event's own cell is pooled with the stamp of the previous
+     * event at its pixel (or farms_serial_first's), and an event with no
+     * contributor takes its own flow at scale 0 (:1085-1094).  0: runFileCopy. */
+    int32_t serial;
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA
@@ -145,6 +151,11 @@ int farms_last_stamps(farms_handle *h, const int32_t *d_x, const int32_t *d_y, c
 int farms_merge_stamps(farms_handle *h, const int64_t *d_in, int32_t count, int64_t *d_out);
 /* Start the handle (fresh or reset) from the SAE d_stamp; flow state stays empty. */
 int farms_seed_sae(farms_handle *h, const int64_t *d_stamp);
+
+/* Serial mode: the file's first line (x, y, absolute stamp t_abs) is not an
+ * event of the loop; it only sets lastEventTime[x][y] = t_abs (vFlow.cpp:531-556).
+ * Call once on a fresh (or reset) serial handle before farms_process. */
+int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_t t_abs);
 
 /* Number of pooling scales, floor(max_window / window_jump) + 1. */
 int farms_num_scales(const farms_handle *h);

@@ -45,6 +45,21 @@ int farms_synth_preset(int config, farms_synth_params *out);
 int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x, int32_t *y,
                              uint32_t *t, int32_t *pol);
 
+/* The events with index in [e0, e1) and column in [x_lo, x_hi) of the stream
+ * farms_synth_generate would produce, in stream order, with their stream
+ * indices in idx (may be NULL), and the stream's first stamp in *t_first (may
+ * be NULL; the t0 of vFlow.cpp:194): one rank's share of a multi-GPU run
+ * without holding the whole stream.  At most cap events are written; returns
+ * how many events match (possibly > cap), or a negative code. */
+int64_t farms_synth_generate_select(const farms_synth_params *p, int64_t e0, int64_t e1,
+                                    int32_t x_lo, int32_t x_hi, int64_t cap, int32_t *x,
+                                    int32_t *y, uint32_t *t, int32_t *pol, int64_t *idx,
+                                    uint32_t *t_first);
+
+/* Events per column (p->width counts) of the whole stream: the balance of a
+ * multi-GPU x-strip plan.  Returns 0 or a negative code. */
+int farms_synth_column_hist(const farms_synth_params *p, int64_t *hist);
+
 /* Write events as the reference's input text format, one "x y t p" line per
  * event (README.md "Input event files").  Returns 0 or -1 on I/O error. */
 int farms_synth_write_text(const char *path, const int32_t *x, const int32_t *y,

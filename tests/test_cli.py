@@ -82,3 +82,17 @@ def test_cli_numevents_caps_input(tmp_path):
     r = run("--filename", base, "--width", "128", "--height", "128", "--numevents", "1234", "--SERIAL", "0")
     assert r.returncode == 0, r.stderr
     assert len(open(base + "_FARMSOut_batch.txt").read().splitlines()) == 1234
+
+
+@pytest.mark.gpu
+def test_cli_serial_mode_runs_the_serial_engine(tmp_path):
+    """--SERIAL 1 (the reference default): vFlowManager::run semantics — the
+    first line only stamps lastEventTime, NUMEVENTS + 1 events are processed
+    (vFlow.cpp:565), nothing is written (the writer is commented out, :487-489)."""
+    ev = farms.synth_config(1, 3000)
+    base = str(tmp_path / "s1")
+    farms.write_events_text(base + ".txt", ev)
+    r = run("--filename", base, "--width", "128", "--height", "128", "--numevents", "2000", "--SERIAL", "1")
+    assert r.returncode == 0, r.stderr
+    assert "Running serially" in r.stdout and f"First time = {int(ev.t[0])}" in r.stdout and "Done!" in r.stdout
+    assert not os.path.exists(base + "_FARMSOut_batch.txt")

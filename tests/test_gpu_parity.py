@@ -251,3 +251,98 @@ def test_full_size_stream_properties():
     r, rc = oracles(x[:k], y[:k], t[:k], p[:k], 720, 1280, 5, 5)
     assert_parity(g, r, 720, 1280, rc=rc)
     assert int((outs[0]["r_local"] > 0).sum()) > n // 4  # most of the stream is pooled
+
+
+@pytest.mark.parametrize("threads,pool_chunk", [("1", 1024), ("3", 2048), ("8", 0)])
+def test_host_path_equals_device_path(threads, pool_chunk, monkeypatch):
+    """farms_process (pinned staging, record downloads overlapped per pooling
+    super-chunk, threaded copy-out) gives bitwise the records of
+    farms_process_device on the same stream, for any thread count and with
+    many super-chunks in flight."""
+    import torch
+
+    monkeypatch.setenv("FARMS_HOST_THREADS", threads)
+    ev = farms.synth_config(3, 3_000_000)
+    x, y, t, p = ev.relative()
+    n = len(x)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(a).to(dev) for a in (x, y, t.view(np.int32), p)]
+    o = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+         for c in farms.COLUMNS[4:]}
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=pool_chunk, pool_batch=8 if pool_chunk else 0) as fm:
+        fm.process_device(*d, o)
+        fm.reset()
+        g = fm.process(x, y, t, p)
+    dd = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
+    dd.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
+    assert bitwise_equal(g, dd)
+
+
+def serial_inputs(ev):
+    """vFlowManager::run's view of a file (vFlow.cpp:520-580): the first line
+    only stamps lastEventTime with its absolute time; the loop's events carry
+    t - t0 (t0 = the first line's stamp) and clamped polarity."""
+    first = (int(ev.x[0]), int(ev.y[0]), int(ev.t[0]))
+    x, y = ev.x[1:].astype(np.int32), ev.y[1:].astype(np.int32)
+    t = (ev.t[1:].astype(np.uint32) - np.uint32(ev.t[0])).astype(np.uint32)
+    p = np.maximum(ev.p[1:], 0).astype(np.int32)
+    return first, x, y, t, p
+
+
+def run_serial(first, x, y, t, p, H, W, fs, inl=5, jump=5, maxw=50, splits=None, **kw):
+    with farms.FlowManager(H, W, fs, inl, window_jump=jump, max_window=maxw, serial=True, **kw) as fm:
+        fm.serial_first(*first)
+        if splits is None:
+            g = fm.process(x, y, t, p)
+        else:
+            parts = [fm.process(x[a:b], y[a:b], t[a:b], p[a:b]) for a, b in splits]
+            g = {c: np.concatenate([getattr(q, c) for q in parts]) for c in farms.COLUMNS}
+    outs = []
+    for libm in ("glibc", "cr"):
+        o = OracleFlow(H, W, fs, inl, jump, maxw, serial=True, libm=libm)
+        o.serial_first(*first)
+        outs.append(o.process(x, y, t, p))
+    return g, outs[0], outs[1]
+
+
+def assert_serial_parity(g, r, rc, H, W, first, jump=5, maxw=50):
+    rep = compare(g, r)
+    pc = pooling_check(g, H, W, jump, maxw, serial=True, first=first)
+    print(rep, pc)
+    assert rep["ok"], rep
+    assert pc["ok"] and pc["scale_mismatch"] == 0, pc
+    assert bitwise_equal(g, rc), compare(g, rc)
+    return rep
+
+
+@pytest.mark.parametrize("cfg,n,fs", [(1, 100_000, 3), (2, 200_000, 5), (3, 150_000, 5), (4, 100_000, 7)])
+def test_serial_mode_vs_oracle(cfg, n, fs):
+    """--SERIAL 1 (vFlowManager::run, the reference CLI's default): own cell
+    pooled with the previous stamp at its pixel, fallback to the own flow when
+    nothing contributes (vFlow.cpp:790, 1085-1094)."""
+    W, H = {1: (128, 128), 2: (320, 320), 3: (1280, 720), 4: (1280, 720)}[cfg]
+    first, x, y, t, p = serial_inputs(farms.synth_config(cfg, n + 1))
+    g, r, rc = run_serial(first, x, y, t, p, H, W, fs)
+    rep = assert_serial_parity(g, r, rc, H, W, first)
+    assert rep["valid_ref"] > n // 20
+
+
+def test_serial_first_line_stamp_and_streaming():
+    """The first line's absolute stamp sits in lastEventTime of its pixel: with a
+    small t0 an early event there pools its own cell against it.  Serial mode
+    is also bitwise invariant to splitting the stream across calls and to the
+    chunk sizes."""
+    ev = farms.synth_config(1, 60_001)
+    t = (ev.t - ev.t[0] + 300).astype(np.uint32)  # t0 = 300
+    ev = farms.Events(ev.x.copy(), ev.y.copy(), t, ev.p.copy())
+    # events 1..40 at the first line's pixel, 10 us apart (relative 0..400)
+    ev.x[1:41], ev.y[1:41] = ev.x[0], ev.y[0]
+    ev.t[1:41] = 300 + 10 * np.arange(40, dtype=np.uint32)
+    order = np.argsort(ev.t, kind="stable")
+    ev = farms.Events(ev.x[order], ev.y[order], ev.t[order], ev.p[order])
+    first, x, y, t, p = serial_inputs(ev)
+    g, r, rc = run_serial(first, x, y, t, p, 128, 128, 3)
+    assert_serial_parity(g, r, rc, 128, 128, first)
+    g2, _, _ = run_serial(first, x, y, t, p, 128, 128, 3, splits=[(0, 7), (7, 20_000), (20_000, len(x))],
+                          fit_chunk=1000, pool_chunk=256)
+    assert bitwise_equal(g, g2)

@@ -195,3 +195,44 @@ def test_chunk_parallel_parse_equals_one_thread(io, seed):
         assert r1[0] == r7[0] == cap
         for a, b in zip(r1[1:], r7[1:]):
             assert np.array_equal(a, b)
+
+
+def parse_serial(io, text: bytes, numevents=1 << 40):
+    io.farms_io_parse_serial.restype = ctypes.c_int64
+    io.farms_io_parse_serial.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64] + [ctypes.c_void_p] * 5 + [
+        ctypes.c_int64]
+    cap = text.count(b"\n") + 2
+    first = np.zeros(4, np.int32)
+    x, y, p = (np.zeros(cap, np.int32) for _ in range(3))
+    t = np.zeros(cap, np.uint32)
+    n = io.farms_io_parse_serial(text, len(text), numevents, first.ctypes.data, x.ctypes.data, y.ctypes.data,
+                                 t.ctypes.data, p.ctypes.data, cap)
+    assert n >= 0
+    f = (int(first[0]), int(first[1]), int(first[2]), int(np.uint32(first[3])))
+    return f, [(int(x[i]), int(y[i]), int(t[i]), int(p[i])) for i in range(n)]
+
+
+def test_serial_parse_first_line_and_relative_time(io):
+    """vFlowManager::run (vFlow.cpp:520-580): line 1 is (x0, y0, t0) only; the
+    loop subtracts t0 and clamps the polarity in place."""
+    f, ev = parse_serial(io, b"3 4 1000 -1\n1 2 1030 -1\n5 6 1050 1\n")
+    assert f == (1, 3, 4, 1000)
+    assert ev == [(1, 2, 30, 0), (5, 6, 50, 1)]
+
+
+def test_serial_parse_carry_subtracts_t0_again(io):
+    """A line without a time field keeps the carried *relative* stamp, from
+    which `time_ = time_ - t0` subtracts t0 once more (uint32 wrap); a missing
+    polarity keeps the clamped one."""
+    f, ev = parse_serial(io, b"0 0 100 1\n1 2 130 -1\n7 8\n")
+    assert ev[0] == (1, 2, 30, 0)
+    assert ev[1] == (7, 8, (30 - 100) % (1 << 32), 0)
+
+
+def test_serial_parse_numevents_cap(io):
+    """while (getline && eventsComputed <= NUMEVENTS): NUMEVENTS + 1 events."""
+    text = b"".join(b"%d 1 %d 1\n" % (i, 100 + i) for i in range(10))
+    _, ev = parse_serial(io, text, numevents=3)
+    assert len(ev) == 4 and ev[-1] == (4, 1, 4, 1)
+    _, ev = parse_serial(io, b"")
+    assert ev == []

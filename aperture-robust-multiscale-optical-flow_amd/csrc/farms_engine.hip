@@ -157,6 +157,8 @@ struct Ctx {
     int64_t nwords;
     int NB, C2;            // ring size, events per pooling chunk
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
+    int pool_ri;           // k_pool_grp: row-info words (rows + 1)
+    const int32_t *gstart; // pooling groups: first work-order position of group g (gstart[G] = n)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): per event, the stamp
     // its pixel's lastEventTime holds while the event is pooled (written only
@@ -243,7 +245,7 @@ __device__ __forceinline__ int work_block() {
 // Validate, pixel id, and the work-order key: (pooling chunk, 8x8 tile) so
 // that the threads of a wave and the waves of a CU work on neighbouring pixels.
 __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int *err, int pool_chunk,
-                       int tile_bits) {
+                       int tile_bits, int tile_shift) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= c.n) return;
     const int x = c.x[e], y = c.y[e];
@@ -253,7 +255,8 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
         pix[e] = 0;
     } else {
         pix[e] = (uint32_t)(x - c.X0) * (uint32_t)c.H + (uint32_t)y;
-        tile = (uint32_t)((x - c.X0) >> 3) * (uint32_t)((c.H + 7) >> 3) + (uint32_t)(y >> 3);
+        const int ts = tile_shift, tm = (1 << ts) - 1;
+        tile = (uint32_t)((x - c.X0) >> ts) * (uint32_t)((c.H + tm) >> ts) + (uint32_t)(y >> ts);
     }
     wkey[e] = ((uint32_t)(e / pool_chunk) << tile_bits) | tile;
     iota[e] = e;
@@ -303,6 +306,29 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
     if (threadIdx.x == 0) {
         tmin[ch] = slo[0];
         tmax[ch] = shi[0];
+    }
+}
+
+// Pooling groups (k_pool_grp): a group starts where the (pooling chunk, tile)
+// key of the work order changes, and at every split-th position inside a run.
+__global__ void k_group_flags(const uint32_t *wkey_sorted, int n, int split, uint8_t *flags) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n) return;
+    flags[w] = (w == 0 || wkey_sorted[w] != wkey_sorted[w - 1] || w % split == 0) ? 1 : 0;
+}
+
+// gstart[G] = n; chunk_g0[ch] = first group of pooling chunk ch (chunk ch
+// holds work-order positions [ch * C2, (ch + 1) * C2): every chunk has groups),
+// chunk_g0[nch] = G.
+__global__ void k_group_index(int n, const int *ng, int32_t *gstart, int C2, int32_t *chunk_g0, int nch) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int G = *ng;
+    if (g >= G) return;
+    const int ch = gstart[g] / C2;
+    if (g == 0 || gstart[g - 1] / C2 != ch) chunk_g0[ch] = g;
+    if (g == 0) {
+        gstart[G] = n;
+        chunk_g0[nch] = G;
     }
 }
 
@@ -1549,23 +1575,20 @@ __device__ __forceinline__ double wave_max(double v) {
 #ifndef FARMS_POOL_UNROLL
 #define FARMS_POOL_UNROLL 8  // phase B entries per loop trip (4 or 8; 64 must be a multiple)
 #endif
-template <int K>
-__device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                           uint64_t *s_start, int2 *s_row, uint2 *s_con, double *s_val,
-                                           uint8_t *s_k0) {
-    static_assert(3 * K <= 64, "one lane per (quantity, scale)");
-    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
-    const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
-    const int W = c.W, H = c.H, M = c.M, J = c.J;
+// Row setup of a pooling window: the flattened candidate slices of rows
+// [i_lo, i_lo + nrows) (nrows <= 128), cells j in [j_lo, j_hi] of each row
+// (x-major; j already clipped to W-1 as vFlow.cpp:1000/1113 do, so for W > H a
+// row runs into the next column; indices >= W*H do not contribute).  Writes
+// s_start (bit f set iff a non-empty row segment starts at flattened position
+// f), s_row (the non-empty segments in order: {row, candidate index - flattened
+// index}) and, when s_rinfo is given, per row r {flattened start, non-empty
+// segments before r} with the totals at r = nrows.  Returns the flattened
+// length.  LDS private to the calling wave.
+__device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_lo, int nrows, int j_lo, int j_hi,
+                                         uint64_t *s_start, int2 *s_row, int2 *s_rinfo) {
+    const int H = c.H;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
     const int WHs = (int)c.WHs;
-    // serial mode: the own cell is pooled with the stamp its lastEventTime still
-    // holds (the previous event's), not the event's own (vFlow.cpp:790 vs :264)
-    const uint32_t own_lin = c.tprev ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
-    const uint32_t own_tprev = c.tprev ? c.tprev[e] : 0u;
-    const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
-    const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    const int nrows = i_hi - i_lo + 1;  // <= 2M+1 <= 127
     // ---- per-row candidate slices: flattened start of each non-empty row as a
     // bit of s_start, and its candidate offset in s_row
     uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
@@ -1634,6 +1657,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         const uint64_t lt = (1ull << lane) - 1;
         const uint64_t b0 = __ballot(n0[hh] > 0), b1 = __ballot(n1[hh] > 0);
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
+        if (s_rinfo && r < nrows) s_rinfo[r] = make_int2(start, idx);
         if (n0[hh] > 0) {
             s_row[idx++] = make_int2(r, a0[hh] - start);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
@@ -1646,11 +1670,41 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         nz += (int)__popcll(b0) + (int)__popcll(b1);
         carry += __builtin_amdgcn_readlane(incl, 63);
     }
+    if (s_rinfo && lane == 0) s_rinfo[nrows] = make_int2(carry, nz);
     // the LDS arrays are private to this wave: a wavefront-scope fence orders
     // the writes above before the reads below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const int total = carry;
+    return carry;
+}
+
+// Pooling of one valid owned event e at (ex, ey, teu) by the calling wave from
+// a row table built by pool_rows (rows from absolute row row_i0): the
+// flattened candidates [f_lo, f_hi) cover the event's window rows, m_lo
+// non-empty segments start before f_lo, and cells outside j in [jlo, jhi] are
+// not in its window (a group's union table is wider than one event's window).
+//   Phase A: lanes scan the candidates 64 at a time (coalesced 16-B headers,
+//   one step ahead in flight), resolve each cell's state as of e, and compact
+//   the contributors (valid flow, |dt| < 500 us) into LDS in raster order.
+//   Phase B: lane g*K + k sums quantity g (L, L cos, L sin) of scale k over the
+//   staged list sequentially, in the reference's raster order (vFlow.cpp:998-
+//   1021): the per-scale sums, means and the first strict maximum are bitwise
+//   those of the reference given the same local flows.
+template <int K>
+__device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
+                                         int row_i0, int f_lo, int f_hi, int m_lo, int jlo, int jhi,
+                                         const uint64_t *s_start, const int2 *s_row, uint2 *s_con, double *s_val,
+                                         uint8_t *s_k0) {
+    static_assert(3 * K <= 64, "one lane per (quantity, scale)");
+    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
+    const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
+    const int H = c.H, J = c.J;
+    const int OFF = c.X0 * c.H;
+    // serial mode: the own cell is pooled with the stamp its lastEventTime still
+    // holds (the previous event's), not the event's own (vFlow.cpp:790 vs :264)
+    const uint32_t own_lin = c.tprev ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
+    const uint32_t own_tprev = c.tprev ? c.tprev[e] : 0u;
+    const int total = f_hi - f_lo;
 #if FARMS_POOL_STOP == 1
     if (lane == 0) c.scale[e] = total;  // ablation: row setup only
     return;
@@ -1664,7 +1718,9 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         // Flattened positions [fw, fw + 64) (fw a multiple of 64, steps in
         // order): lane f's segment is the last non-empty one starting at or
         // before f, i.e. the (number of segment starts <= f)-th one.
-        int mbase = 0;  // non-empty segments starting before fw
+        const int fw0 = f_lo & ~63;
+        // non-empty segments starting before fw: m_lo less those in [fw0, f_lo)
+        int mbase = m_lo - (int)__popcll(s_start[fw0 >> 6] & ((1ull << (f_lo & 63)) - 1));
         auto locate = [&](int fw, int f, int &row, int &k) {
             const uint64_t mk = s_start[fw >> 6];
             const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
@@ -1677,15 +1733,15 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
         // is resolved
         int rc = 0, kc = 0;
         CandHdr hc{};
-        if (total > 0) { locate(0, lane, rc, kc); if (lane < total) hc = chdr[kc]; }
-        for (int f0 = 0; f0 < total; f0 += 64) {
+        if (f_hi > f_lo) { locate(fw0, fw0 + lane, rc, kc); if (fw0 + lane >= f_lo && fw0 + lane < f_hi) hc = chdr[kc]; }
+        for (int f0 = fw0; f0 < f_hi; f0 += 64) {
             const int f = f0 + lane, fn = f + 64;
             int rn = 0, kn = 0;
             CandHdr hn{};
-            if (f0 + 64 < total) { locate(f0 + 64, fn, rn, kn); if (fn < total) hn = chdr[kn]; }
+            if (f0 + 64 < f_hi) { locate(f0 + 64, fn, rn, kn); if (fn < f_hi) hn = chdr[kn]; }
             bool con = false;
             uint32_t ref = 0, meta = 0;
-            if (f < total) {
+            if (f >= f_lo && f < f_hi) {
                 uint32_t tq, kind;
                 bool ok;
                 if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; kind = 0; ref = (uint32_t)kc; }
@@ -1699,9 +1755,9 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
                 if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
                 // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
                 const int64_t dt = (int64_t)teu - (int64_t)tq;
-                if (ok && (uint64_t)(dt + 499) < 999u) {
-                    const int i = i_lo + rc;
-                    const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
+                const int i = row_i0 + rc;
+                const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
+                if (ok && (uint64_t)(dt + 499) < 999u && j >= jlo && j <= jhi) {
                     const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
                     const int d = di > dj ? di : dj;
                     // smallest scale containing the cell: ceil(d / J)
@@ -1837,6 +1893,18 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     }
 }
 
+// Per-event pooling: the row table of the event's own window, then the event.
+template <int K>
+__device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
+                                           uint64_t *s_start, int2 *s_row, uint2 *s_con, double *s_val,
+                                           uint8_t *s_k0) {
+    const int W = c.W, M = c.M;
+    const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
+    const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
+    const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nullptr);
+    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, 0, total, 0, j_lo, j_hi, s_start, s_row, s_con, s_val, s_k0);
+}
+
 // One wavefront per work-order position of [c0, c1) (events of a chunk in
 // tile order); invalid events and halo events (fitted here, pooled by their
 // owner) leave at once.
@@ -1870,6 +1938,84 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + kPoolCap);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
     pool_event<K>(c, e, ex, ey, teu, buf, lane, s_start, s_row, s_con, s_val, s_k0);
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Group pooling: one wavefront per pooling group, a run of work-order
+// positions with the same (pooling chunk, tile) key (split every
+// c.group_split positions).  The events of a group sit within one tile, so
+// their windows share almost every row: the wave builds the row table of the
+// union of its valid owned events' windows once (pool_rows), then pools each
+// of those events from it (pool_one restricted to the event's rows and
+// columns).  Same contributor lists in the same order as per-event pooling:
+// bitwise the same records.  Requires 2M + tile <= 128 union rows.
+template <int K>
+__global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool_grp(Ctx c, int g0, int g1) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
+    const int nbw = c.pool_bw, nrs = c.pool_rs, nri = c.pool_ri;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g = g0 + work_block() * 4 + wv;
+    if (g >= g1) return;
+    const int ws = c.gstart[g], we = c.gstart[g + 1];
+    const int W = c.W, M = c.M;
+    // union of the windows of the group's valid owned events
+    int xmn = INT_MAX, xmx = INT_MIN, ymn = INT_MAX, ymx = INT_MIN;
+    bool any = false;
+    for (int w0 = ws; w0 < we; w0 += 64) {
+        const int w = w0 + lane;
+        uint32_t vld = 0;
+        int ex = 0, ey = 0;
+        if (w < we) {
+            const int e = c.Q[w];
+            vld = c.valid[e]; ex = c.x[e]; ey = c.y[e];
+        }
+        const bool ok = vld && ex >= c.own_lo && ex < c.own_hi;
+        if (ok) { xmn = min(xmn, ex); xmx = max(xmx, ex); ymn = min(ymn, ey); ymx = max(ymx, ey); }
+        any = any || __ballot(ok) != 0;
+    }
+    if (!any) return;
+    xmn = wave_min_i(xmn); xmx = wave_max_i(xmx); ymn = wave_min_i(ymn); ymx = wave_max_i(ymx);
+    const int i_lo = max(0, xmn - M), i_hi = min(W - 1, xmx + M);
+    const int j_lo = max(0, ymn - M), j_hi = min(W - 1, ymx + M);
+    const int buf = (ws / c.C2) % c.NB;
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + nri + kPoolCap + kPoolValWords);
+    int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
+    int2 *s_rinfo = reinterpret_cast<int2 *>(s_start + nbw + nrs);
+    uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs + nri);
+    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + nri + kPoolCap);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
+    pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, s_rinfo);
+    for (int w0 = ws; w0 < we; w0 += 64) {
+        const int w = w0 + lane;
+        uint32_t vld = 0, te = 0;
+        int e = 0, ex = 0, ey = 0;
+        if (w < we) {
+            e = c.Q[w];
+            vld = c.valid[e]; ex = c.x[e]; ey = c.y[e]; te = c.t[e];
+        }
+        uint64_t bal = __ballot(vld && ex >= c.own_lo && ex < c.own_hi);
+        while (bal) {
+            const int l = __builtin_ctzll(bal);
+            bal &= bal - 1;
+            const int el = __builtin_amdgcn_readlane(e, l), xl = __builtin_amdgcn_readlane(ex, l),
+                      yl = __builtin_amdgcn_readlane(ey, l);
+            const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)te, l);
+            const int r0 = max(xl - M, i_lo) - i_lo, r1 = min(xl + M, i_hi) - i_lo;
+            const int2 a = s_rinfo[r0], b = s_rinfo[r1 + 1];
+            pool_one<K>(c, el, xl, yl, tl, buf, lane, i_lo, a.x, b.x, a.y, max(0, yl - M), min(W - 1, yl + M),
+                        s_start, s_row, s_con, s_val, s_k0);
+        }
+    }
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -2014,6 +2160,14 @@ struct farms_handle {
     uint32_t first_t = 0;
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     int tile_bits = 0;
+    int tile_shift = 3;       // work-order tile: 2^tile_shift square (FARMS_POOL_TILE)
+    bool pool_groups = false; // FARMS_POOL_GROUPS=1: k_pool_grp (measured 1.5x slower than per-event
+                              // k_pool at C3, DESIGN.md §8: fewer resident waves, events serial per wave)
+    int group_split = 64;    // work-order positions per pooling group at most (FARMS_GROUP_SPLIT)
+    uint8_t *gflags = nullptr;
+    int32_t *gstart = nullptr, *chunk_g0 = nullptr;
+    int *d_ng = nullptr;
+    std::vector<int32_t> chunk_g0_h;
     uint8_t *valid = nullptr;
     FlowCell *evf = nullptr;
     int2 *dbg_tc = nullptr;
@@ -2057,6 +2211,7 @@ void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->pos); dfree(h->prev); dfree(h->next);
     dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted); dfree(h->tprev);
+    dfree(h->gflags); dfree(h->gstart); dfree(h->chunk_g0); dfree(h->d_ng);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2083,7 +2238,9 @@ int ensure_capacity(farms_handle *h, int64_t n) {
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
-        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap)))) {
+        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap))) ||
+        (rc = dalloc(&h->gflags, cap)) || (rc = dalloc(&h->gstart, cap + 1)) || (rc = dalloc(&h->chunk_g0, nch + 1)) ||
+        (rc = dalloc(&h->d_ng, 1))) {
         free_workspace(h);
         return rc;
     }
@@ -2094,7 +2251,10 @@ int ensure_capacity(farms_handle *h, int64_t n) {
                                               end_bit_for(h->WH), h->stream));
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, h->wkey, h->wkey_sorted, h->iota, h->Q, (int)cap, 0,
                                               32, h->stream));
-    bytes = std::max(bytes, bytes2);
+    size_t bytes3 = 0;
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, bytes3, hipcub::CountingInputIterator<int32_t>(0), h->gflags,
+                                         h->gstart, h->d_ng, (int)cap, h->stream));
+    bytes = std::max(bytes, std::max(bytes2, bytes3));
     if ((rc = dalloc((uint8_t **)&h->cub_tmp, bytes))) { free_workspace(h); return rc; }
     h->cub_bytes = bytes;
     h->cap = cap;
@@ -2121,7 +2281,24 @@ void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), lds, s, c, c0, c1);
 }
 
+template <int K>
+void launch_pool_grp(const Ctx &c, int g0, int g1, hipStream_t s) {
+    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + c.pool_ri + kPoolCap + kPoolValWords);
+    if (g1 > g0) hipLaunchKernelGGL(k_pool_grp<K>, dim3(ceil_div(g1 - g0, 4)), dim3(256), lds, s, c, g0, g1);
+}
+
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
+pool_launcher pool_grp_for(int K) {
+    switch (K) {
+    case 1: return launch_pool_grp<1>;   case 2: return launch_pool_grp<2>;   case 3: return launch_pool_grp<3>;
+    case 4: return launch_pool_grp<4>;   case 5: return launch_pool_grp<5>;   case 6: return launch_pool_grp<6>;
+    case 7: return launch_pool_grp<7>;   case 8: return launch_pool_grp<8>;   case 9: return launch_pool_grp<9>;
+    case 10: return launch_pool_grp<10>; case 11: return launch_pool_grp<11>; case 12: return launch_pool_grp<12>;
+    case 13: return launch_pool_grp<13>; case 14: return launch_pool_grp<14>; case 15: return launch_pool_grp<15>;
+    case 16: return launch_pool_grp<16>;
+    default: return nullptr;
+    }
+}
 pool_launcher pool_for(int K) {
     switch (K) {
     case 1: return launch_pool<1>;   case 2: return launch_pool<2>;   case 3: return launch_pool<3>;
@@ -2201,8 +2378,12 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.bm_ring = h->bm_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
-    c.pool_bw = ((2 * h->M + 1) * (2 * h->M + 1) + 63) / 64;  // flattened window positions
-    c.pool_rs = 2 * (2 * h->M + 1);                             // <= 2 segments per window row
+    // a group's union window spans <= 2M + 2^tile_shift rows and columns
+    const int span = h->pool_groups ? 2 * h->M + (1 << h->tile_shift) : 2 * h->M + 1;
+    c.pool_bw = (span * span + 63) / 64;  // flattened window positions
+    c.pool_rs = 2 * span;                 // <= 2 segments per window row
+    c.pool_ri = h->pool_groups ? span + 1 : 0;
+    c.gstart = h->gstart;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
@@ -2233,7 +2414,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
     HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->wkey, h->err,
-                       h->pool_chunk, h->tile_bits);
+                       h->pool_chunk, h->tile_bits, h->tile_shift);
     int herr = 0;
     HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -2253,6 +2434,19 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
                                                   h->tile_bits + cb, s));
     }
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
+    if (h->pool_groups) {  // pooling groups and each pooling chunk's first group (read back: launch bounds)
+        hipLaunchKernelGGL(k_group_flags, dim3(ceil_div(n, 256)), dim3(256), 0, s, h->wkey_sorted, n, h->group_split,
+                           h->gflags);
+        size_t b3 = h->cub_bytes;
+        HIPCHK(hipcub::DeviceSelect::Flagged(h->cub_tmp, b3, hipcub::CountingInputIterator<int32_t>(0), h->gflags,
+                                             h->gstart, h->d_ng, n, s));
+        hipLaunchKernelGGL(k_group_index, dim3(ceil_div(n, 256)), dim3(256), 0, s, n, h->d_ng, h->gstart, h->pool_chunk,
+                           h->chunk_g0, n_pool_chunks);
+        h->chunk_g0_h.resize((size_t)n_pool_chunks + 1);
+        HIPCHK(hipMemcpyAsync(h->chunk_g0_h.data(), h->chunk_g0, sizeof(int32_t) * (n_pool_chunks + 1),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
 
@@ -2270,7 +2464,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const char *ser = getenv("FARMS_SERIALIZE");
     const bool serial = ser && ser[0] == '1';
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
-    pool_launcher pl = pool_for(h->K);
+    pool_launcher pl = h->pool_groups ? pool_grp_for(h->K) : pool_for(h->K);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
     const bool fit_quad = !(fq && fq[0] == '0');
@@ -2320,7 +2514,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
-        pl(c, p0, p1, sp);
+        if (h->pool_groups) pl(c, h->chunk_g0_h[ch0], h->chunk_g0_h[ch1], sp);
+        else pl(c, p0, p1, sp);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
         hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
@@ -2457,8 +2652,13 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->cstride = (int64_t)h->nblk * kGroupCells;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
+    if (const char *v = getenv("FARMS_POOL_TILE")) h->tile_shift = std::max(1, std::min(atoi(v), 6));
+    if (const char *v = getenv("FARMS_GROUP_SPLIT")) h->group_split = std::max(1, atoi(v));
+    if (const char *v = getenv("FARMS_POOL_GROUPS")) h->pool_groups = v[0] != '0';
+    if (2 * h->M + (1 << h->tile_shift) > 128) h->pool_groups = false;  // union rows: 2 per lane
     {
-        const int64_t tiles = (int64_t)((h->W + 7) >> 3) * ((h->H + 7) >> 3);
+        const int tm = (1 << h->tile_shift) - 1;
+        const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);
         while ((int64_t(1) << h->tile_bits) < tiles) ++h->tile_bits;
     }
     int rc = FARMS_OK;

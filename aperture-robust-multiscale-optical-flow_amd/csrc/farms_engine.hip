@@ -130,6 +130,8 @@ struct Ctx {
     int64_t WHs;           // cells of the whole sensor (W x H): the pooling window's end
     int X0, XR1;           // stored region: columns [X0, XR1); cell index = (x - X0) * H + y
     int own_lo, own_hi;    // pooled (owned) columns [own_lo, own_hi)
+    int fit_lo, fit_hi;    // fitted columns: all stored ones, or (import_halo) the owned ones
+    bool fit_all;          // fit_lo / fit_hi cover the stored region (no per-event test)
     int fr, min_inl, J, M;
     float invJ;            // 1/J: scale index of a cell = floor((d + J - 1 + 0.5) * invJ)
     const int32_t *x, *y, *p;
@@ -747,6 +749,10 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
     const int w = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c1) return;
     const int e = c.Q[w];  // chunk [c0, c1) occupies positions [c0, c1) of Q
+    if (!c.fit_all) {
+        const int ex = c.x[e];
+        if (ex < c.fit_lo || ex >= c.fit_hi) return;
+    }
     double vx, vy;
     fit_event_fast<FR>(c, e, seq, s_tk + threadIdx.x, vx, vy);
     fit_store(c, e, vx, vy);
@@ -1155,6 +1161,10 @@ __global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
     const int e = c.Q[w];
+    if (!c.fit_all) {  // halo columns: flows come from their owner (farms_import_flows)
+        const int ex = c.x[e];
+        if (ex < c.fit_lo || ex >= c.fit_hi) return;  // the whole quad
+    }
     double vx, vy;
     if constexpr (UT) fit_event_quad_u<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
     else fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
@@ -1331,6 +1341,10 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
     const int n = count;
     const int stride = (int)gridDim.x * 4;
     for (int i = (int)blockIdx.x * 4 + wv; i < n; i += stride) {
+        if (!c.fit_all) {
+            const int ex = c.x[list[i]];
+            if (ex < c.fit_lo || ex >= c.fit_hi) continue;  // wave-uniform
+        }
         fit_wave_event(c, list[i], seq, s_t[wv], s_v[wv], lane);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -2031,6 +2045,34 @@ __global__ void k_true_polar(Ctx c, int e0, int e1) {
 }
 
 // ---------------------------------------------------------------------------
+// x-strips with a flow-halo exchange (multi-GPU): the local flows
+// {L, L cos(theta), L sin(theta)} of listed events out of / into evf.  An
+// imported flow takes the local event's stamp; validity is L > 0 (the gate's
+// L = 0 for an invalid event, vFlow.cpp:398-402).
+__global__ void k_export_flows(const FlowCell *evf, const int32_t *idx, int count, double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const FlowCell f = evf[idx[i]];
+    out[3 * (int64_t)i] = f.L;
+    out[3 * (int64_t)i + 1] = f.Lc;
+    out[3 * (int64_t)i + 2] = f.Ls;
+}
+
+__global__ void k_import_flows(Ctx c, const int32_t *idx, int count, const double *in) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int e = idx[i];
+    FlowCell f;
+    f.L = in[3 * (int64_t)i];
+    f.Lc = in[3 * (int64_t)i + 1];
+    f.Ls = in[3 * (int64_t)i + 2];
+    f.t = c.t[e];
+    f.pad = 0;
+    c.evf[e] = f;
+    c.valid[e] = f.L > 0 ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
 // Temporal segments (multi-GPU): the SAE a segment starts from.
 // Last event index per pixel (x-major, whole sensor), then its stamp.
 __global__ void k_last_index(const int32_t *x, const int32_t *y, int e0, int e1, int W, int H, int32_t *last) {
@@ -2156,6 +2198,11 @@ struct farms_handle {
     int32_t *iota = nullptr, *P = nullptr, *pos = nullptr, *prev = nullptr, *next = nullptr;
     int32_t *Q = nullptr;
     uint32_t *tprev = nullptr;  // serial mode only
+    // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
+    const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
+    const uint32_t *ph_t = nullptr;
+    int64_t ph_n = -1;
+    farms_records ph_out{};
     int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
     uint32_t first_t = 0;
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
@@ -2358,14 +2405,20 @@ int ensure_sync_events(farms_handle *h, size_t count) {
 // null) is called as soon as the work of pooling super-chunk S (events [p0,
 // p1)) is enqueued, with the event that marks its records final on the device:
 // the host-array path starts the download of those records there.
+// phase 0 runs the whole loop; phase 1 only prep and the local fits (then
+// synchronizes), phase 2 only the pooling sweep of the events phase 1 saw: the
+// x-strip exchange of halo flows (farms_import_flows) goes between the two.
 typedef std::function<int(int S, int p0, int p1, hipEvent_t done)> super_hook;
 int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
-             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr) {
+             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0) {
     const int n = (int)n64;
     hipStream_t s = h->stream;
     Ctx c{};
     c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH; c.WHs = (int64_t)h->W * h->H;
     c.X0 = h->X0; c.XR1 = h->X0 + h->WR; c.own_lo = h->own_lo; c.own_hi = h->own_hi;
+    c.fit_lo = h->prm.import_halo ? h->own_lo : h->X0;
+    c.fit_hi = h->prm.import_halo ? h->own_hi : h->X0 + h->WR;
+    c.fit_all = c.fit_lo <= h->X0 && c.fit_hi >= h->X0 + h->WR;
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
@@ -2412,6 +2465,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     auto ev_pool = [&](int S) { return h->sync_ev[2 + n_fit_chunks + 2 * S]; };
 
     // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
+    if (phase == 2) {  // prepared by phase 1
+        if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
+        HIPCHK(hipEventRecord(ev_prep, s));
+    } else {
     HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->wkey, h->err,
                        h->pool_chunk, h->tile_bits, h->tile_shift);
@@ -2449,6 +2506,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     }
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
+    }  // prep
 
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
@@ -2494,6 +2552,20 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     };
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     int fit_enqueued = 0, fit_waited = -1;
+    if (phase == 1) {  // the whole fit sweep, then back to the caller
+        while (fit_enqueued < n_fit_chunks) {
+            int rc = enqueue_fit(fit_enqueued++);
+            if (rc) return rc;
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipGetLastError());
+        farms_stats st{};
+        st.n_events = n;
+        st.fit_launches = fit_launches;
+        h->stats = st;
+        return FARMS_OK;
+    }
+    if (phase == 2) { fit_enqueued = n_fit_chunks; fit_waited = n_fit_chunks - 1; }  // fits done (phase 1)
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
         // keep the fit sweep one super-chunk ahead of the chain
@@ -2814,6 +2886,68 @@ extern "C" int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_
                      hipMemcpyHostToDevice));
     h->first_q = (int64_t)x * h->H + y;
     h->first_t = t_abs;
+    return FARMS_OK;
+}
+
+namespace {
+int check_device_call(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
+                      const int32_t *d_p, int64_t n, const farms_records *d_out) {
+    if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
+    if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
+    if (n > 0 && (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx ||
+                  !d_out->vy || !d_out->r_local || !d_out->theta_local || !d_out->scale))
+        return fail(FARMS_EINVAL, "null array");
+    return FARMS_OK;
+}
+}  // namespace
+
+extern "C" int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
+                                const int32_t *d_p, int64_t n, farms_records *d_out) {
+    int rc = check_device_call(h, d_x, d_y, d_t, d_p, n, d_out);
+    if (rc) return rc;
+    h->ph_n = -1;
+    if (n == 0) return FARMS_OK;
+    HIPCHK(hipSetDevice(h->prm.device));
+    if ((rc = ensure_capacity(h, n))) return rc;
+    if ((rc = run_core(h, d_x, d_y, d_t, d_p, n, d_out, nullptr, 1))) return rc;
+    h->ph_x = d_x; h->ph_y = d_y; h->ph_t = d_t; h->ph_p = d_p; h->ph_n = n; h->ph_out = *d_out;
+    return FARMS_OK;
+}
+
+extern "C" int farms_pool_device(farms_handle *h) {
+    if (!h) return fail(FARMS_EINVAL, "null handle");
+    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_pool_device without a preceding farms_fit_device");
+    HIPCHK(hipSetDevice(h->prm.device));
+    const int64_t n = h->ph_n;
+    h->ph_n = -1;
+    return run_core(h, h->ph_x, h->ph_y, h->ph_t, h->ph_p, n, &h->ph_out, nullptr, 2);
+}
+
+extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
+    if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
+        return fail(FARMS_EINVAL, "bad argument");
+    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_export_flows outside a fit / pool pair");
+    HIPCHK(hipSetDevice(h->prm.device));
+    if (count > 0)
+        hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->evf, d_idx,
+                           (int)count, d_flows);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipGetLastError());
+    return FARMS_OK;
+}
+
+extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows) {
+    if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
+        return fail(FARMS_EINVAL, "bad argument");
+    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_import_flows outside a fit / pool pair");
+    HIPCHK(hipSetDevice(h->prm.device));
+    Ctx c{};
+    c.t = h->ph_t; c.evf = h->evf; c.valid = h->valid;
+    if (count > 0)
+        hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, c, d_idx, (int)count,
+                           d_flows);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipGetLastError());
     return FARMS_OK;
 }
 

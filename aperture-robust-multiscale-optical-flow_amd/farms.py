@@ -56,6 +56,7 @@ class FarmsParams(ctypes.Structure):
         ("own_x1", ctypes.c_int32),
         ("pool_batch", ctypes.c_int32),
         ("serial", ctypes.c_int32),
+        ("import_halo", ctypes.c_int32),
     ]
 
 
@@ -110,7 +111,8 @@ HIP_SYMBOLS = (
     "farms_default_params", "farms_create", "farms_destroy", "farms_reset", "farms_process",
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
     "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
-    "farms_seed_sae", "farms_serial_first",
+    "farms_seed_sae", "farms_serial_first", "farms_fit_device", "farms_pool_device", "farms_export_flows",
+    "farms_import_flows",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text",
                  "farms_synth_generate_select", "farms_synth_column_hist")
@@ -326,7 +328,7 @@ class FlowManager:
     def __init__(self, height: int = 320, width: int = 320, filter_size: int = 3, min_evts_on_plane: int = 5,
                  window_jump: int = 5, max_window: int = 50, device: int = 0, fit_chunk: int = 0,
                  pool_chunk: int = 0, region: tuple | None = None, owned: tuple | None = None,
-                 pool_batch: int = 0, serial: bool = False):
+                 pool_batch: int = 0, serial: bool = False, import_halo: bool = False):
         self._lib = load_hip_library()
         prm = FarmsParams()
         _check(self._lib, self._lib.farms_default_params(ctypes.byref(prm)))
@@ -336,6 +338,7 @@ class FlowManager:
         prm.device, prm.fit_chunk, prm.pool_chunk = int(device), int(fit_chunk), int(pool_chunk)
         prm.pool_batch = int(pool_batch)
         prm.serial = 1 if serial else 0
+        prm.import_halo = 1 if import_halo else 0
         if region is not None:  # (x0, x1): stored columns
             prm.region_x0, prm.region_width = int(region[0]), int(region[1]) - int(region[0])
         if owned is not None:  # (x0, x1): pooled columns
@@ -424,6 +427,39 @@ class FlowManager:
     def seed_sae(self, stamp) -> None:
         """Start this (fresh or reset) handle from the SAE surface `stamp`."""
         _check(self._lib, self._lib.farms_seed_sae(self._h, ctypes.c_void_p(stamp.data_ptr())))
+
+    # ---- x-strips with a flow-halo exchange (strips.py, DESIGN.md §6)
+    def fit_device(self, x, y, t_rel, p, out: dict) -> None:
+        """Phase 1 of process_device: prep and the local fits (owned columns
+        only with import_halo).  Then export_flows / import_flows, then
+        pool_device()."""
+        n = int(x.shape[0])
+        rec = self._device_records(out)
+        _check(self._lib, self._lib.farms_fit_device(
+            self._h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(t_rel.data_ptr()),
+            ctypes.c_void_p(p.data_ptr()), ctypes.c_int64(n), ctypes.byref(rec)))
+
+    def export_flows(self, idx, flows) -> None:
+        """flows[i] = {L, L cos theta, L sin theta} of event idx[i] (device int32 /
+        float64 (count, 3) tensors)."""
+        _check(self._lib, self._lib.farms_export_flows(self._h, ctypes.c_void_p(idx.data_ptr()),
+                                                       ctypes.c_int64(int(idx.shape[0])),
+                                                       ctypes.c_void_p(flows.data_ptr())))
+
+    def import_flows(self, idx, flows) -> None:
+        """Set the local flows of events idx (their owners' export_flows)."""
+        _check(self._lib, self._lib.farms_import_flows(self._h, ctypes.c_void_p(idx.data_ptr()),
+                                                       ctypes.c_int64(int(idx.shape[0])),
+                                                       ctypes.c_void_p(flows.data_ptr())))
+
+    def pool_device(self) -> None:
+        """Phase 2: the pooling sweep of the events of the last fit_device."""
+        _check(self._lib, self._lib.farms_pool_device(self._h))
+
+    @staticmethod
+    def _device_records(out: dict) -> FarmsRecordsC:
+        ptr = {c: (ctypes.c_void_p(out[c].data_ptr()) if c in out else None) for c in COLUMNS}
+        return FarmsRecordsC(*[ptr[c] for c in COLUMNS])
 
     def process_device(self, x, y, t_rel, p, out: dict) -> None:
         """Device-resident variant: torch tensors (int32 x/y/p, int32 view of the

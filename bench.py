@@ -55,8 +55,9 @@ def parse():
     ap.add_argument("--pool-chunk", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split", choices=("segments", "strips"), default="segments",
-                    help="N > 1: temporal segments (time-ordered streams) or x-strips")
+    ap.add_argument("--split", choices=("segments", "strips", "strips-recompute"), default="segments",
+                    help="N > 1: temporal segments (time-ordered streams), x-strips with an RCCL exchange of "
+                         "halo flows, or x-strips that recompute their halos")
     ap.add_argument("--host-steps", type=int, default=2,
                     help="N=1: steps of the host-array path (farms_process: H2D + kernels + D2H) timed after "
                          "the device-resident ones (0 = skip)")
@@ -231,12 +232,20 @@ def rank_share(args, cfg: int, world: int, rank: int) -> dict:
                          f"surfaces are all-gathered and each rank starts from the merged SAE plus a re-fitted "
                          f"500 us warm-up ({seg.n_warm} events on rank {rank})"))
     else:
-        strip = strips.plan_hist(farms.synth_column_hist(sp), world, fs, maxw)[rank]
+        exch = args.split == "strips"
+        plan = strips.plan_hist(farms.synth_column_hist(sp), H, world, fs, maxw, exchange=exch)
+        strip = plan[rank]
         ev, _, t_first = farms.synth_select(sp, 0, n, strip.reg_lo, strip.reg_hi)
         sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative(t_first)
-        sh.update(split="strips", region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi),
-                  n_owned=int(strips.owned_mask(sh["x"], strip).sum()),
-                  label=f"{world} x-strips, halo {strips.halo(fs, maxw)} columns recomputed, no data-path collective")
+        hl, hr = strips.halo(fs, maxw, W, H, exchange=exch)
+        sh.update(split=args.split, region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi),
+                  n_owned=int(strips.owned_mask(sh["x"], strip).sum()))
+        if exch:
+            sh["lists"] = strips.exchange_lists(sh["x"], plan, rank)
+            sh["label"] = (f"{world} x-strips: each rank fits its owned columns and, per step, sends the local flows "
+                           f"of its events in other ranks' halos ({hl} / {hr} columns) with one grouped send/recv")
+        else:
+            sh["label"] = f"{world} x-strips, halos of {hl} / {hr} columns recomputed, no data-path collective"
     return sh
 
 
@@ -297,8 +306,19 @@ def main():
     dp = torch.from_numpy(p).to(dev)
     out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
            for c in farms.COLUMNS[4:]}
+    lists = sh.get("lists")
     fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=sh["region"], owned=sh["owned"])
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=sh["region"], owned=sh["owned"],
+                           import_halo=lists is not None)
+    if lists is not None:  # flow-halo exchange buffers, per peer
+        xdev = dev if backend == "nccl" else torch.device("cpu")
+        send_idx = {q: torch.from_numpy(a).to(dev) for q, (a, _) in lists.items()}
+        recv_idx = {q: torch.from_numpy(b).to(dev) for q, (_, b) in lists.items()}
+        send_buf = {q: torch.empty((len(a), 3), dtype=torch.float64, device=dev) for q, (a, _) in lists.items()}
+        recv_buf = {q: torch.empty((len(b), 3), dtype=torch.float64, device=dev) for q, (_, b) in lists.items()}
+        send_x = send_buf if xdev == dev else {q: v.cpu() for q, v in send_buf.items()}
+        recv_x = recv_buf if xdev == dev else {q: v.cpu() for q, v in recv_buf.items()}
+        n_halo_flows = sum(len(b) for _, b in lists.values())
     if seg is not None:  # stamp surfaces: this rank's [head, full], everyone's, the merged SAE
         n_head = sh["n_head"]
         WHs = W * H
@@ -312,6 +332,20 @@ def main():
 
     def step():
         fm.reset()
+        if lists is not None:
+            fm.fit_device(dx, dy, dt_, dp, out)
+            for q in lists:
+                fm.export_flows(send_idx[q], send_buf[q])
+                if send_x[q] is not send_buf[q]:
+                    send_x[q].copy_(send_buf[q])
+            strips.exchange(dist, lists, send_x, recv_x)
+            torch.cuda.synchronize()
+            for q in lists:
+                if recv_x[q] is not recv_buf[q]:
+                    recv_buf[q].copy_(recv_x[q])
+                fm.import_flows(recv_idx[q], recv_buf[q])
+            fm.pool_device()
+            return
         if seg is not None:
             fm.last_stamps(dx[o:], dy[o:], dt_[o:], n_head, mine[0], mine[1])
             dist.all_gather_into_tensor(gath, mine if red_dev == dev else mine.cpu())
@@ -325,6 +359,8 @@ def main():
     # HIP events around the k_pool launches (and phases) only; set before the
     # warmup so that the timed steps replay the launch graph the warmup captured
     fm.set_profiling(farms.PROF_POOL)
+    if dist:
+        dist.barrier()  # communicators up on every rank before the first exchange
     for _ in range(args.warmup):
         step()
     stats = []
@@ -387,6 +423,8 @@ def main():
     if world > 1:
         line["detail"]["rank0_stored_events"] = n
         line["detail"]["rank0_owned_events"] = n_owned
+        if lists is not None:
+            line["detail"]["rank0_halo_flows_received"] = n_halo_flows
     fm.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -63,6 +63,14 @@ typedef struct {
      * event at its pixel (or farms_serial_first's), and an event with no
      * contributor takes its own flow at scale 0 (:1085-1094).  0: runFileCopy. */
     int32_t serial;
+    /* 1: fit only the owned columns [own_x0, own_x1); the local flows of the
+     * other stored events (the halo) are supplied by their owners through
+     * farms_import_flows between farms_fit_device and farms_pool_device
+     * (x-strips with a flow-halo exchange).  The stored region
+     * must then cover the owned columns widened by max_window on the left and
+     * max_window + floor(min(height - 1 + max_window, width - 1) / height) on the
+     * right (the pooling window with the W-1 clip of vFlow.cpp:1000/1113). */
+    int32_t import_halo;
 } farms_params;
 
 /* One output record per input event, the 11 columns of vFlow.cpp:438 in SoA
@@ -115,6 +123,20 @@ int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uin
 int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
                          const uint32_t *d_t_rel, const int32_t *d_p, int64_t n,
                          farms_records *d_out);
+
+/* The per-event loop split at its one exchange point (x-strips):
+ * farms_fit_device runs prep and the local fits (of the owned columns when
+ * import_halo is set) over n device events; farms_export_flows /
+ * farms_import_flows move the flows {L, L cos theta, L sin theta} (3 doubles
+ * per listed event, d_idx = indices into those n events) out of / into the
+ * handle; farms_pool_device then runs the pooling sweep over the same events
+ * into the same records.  Equivalent to farms_process_device when nothing is
+ * imported.  Records of non-owned events are left unspecified. */
+int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t_rel,
+                     const int32_t *d_p, int64_t n, farms_records *d_out);
+int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows);
+int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows);
+int farms_pool_device(farms_handle *h);
 
 /* Profiling of the next calls: FARMS_PROF_TIMING records HIP events around the
  * phases and every k_fit / k_pool launch (times in farms_stats; ~1,700 event

@@ -72,6 +72,6 @@ def test_plan_rank_matches_the_whole_stream_plan(n_seg):
 
 def test_strip_plan_from_histogram_equals_plan_from_events():
     ev = farms.synth_config(2, 100_000)
-    a = strips.plan(ev.x, 320, 4, 5, 50)
-    b = strips.plan_hist(np.bincount(ev.x, minlength=320), 4, 5, 50)
+    a = strips.plan(ev.x, 320, 320, 4, 5, 50)
+    b = strips.plan_hist(np.bincount(ev.x, minlength=320), 320, 4, 5, 50)
     assert a == b

@@ -113,6 +113,14 @@ struct __attribute__((aligned(16))) CandHdr {
     int32_t e1;    // first in-chunk event at the cell, INT_MAX if untouched
     uint32_t t_snap, t1;
 };
+// One 64-cell word of a chunk's candidate bitmap with the candidate index of
+// its first candidate: one 16-B load per lookup (k_pool's row setup reads three
+// per window row, scattered over the window's columns).
+struct __attribute__((aligned(16))) BmWord {
+    uint64_t bm;
+    uint32_t wo;
+    uint32_t pad;
+};
 struct CandVal {
     double L_snap, Lc_snap, Ls_snap;
     double L1, Lc1, Ls1;
@@ -121,6 +129,17 @@ struct CandVal {
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
+// LDS packing of k_pool's row segments and staged contributors (32 bits each):
+//   row segment  = row << 25 | (candidate index - flattened index + kRowBias)
+//   contributor  = k0 << 27 | kind << 25 | ref (kinds 0/1: candidate index;
+//                  kind 2: event id - the chunk's first event id)
+// valid while candidate slots (and pooling chunks) stay below 2^24
+constexpr int kRowBias = 1 << 14;  // flattened positions of a window < 128 x 128
+constexpr uint32_t kRefMask = (1u << 25) - 1;
+constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
+__device__ __forceinline__ uint32_t pack_con(uint32_t ref, uint32_t kind, uint32_t k0) {
+    return (k0 << 27) | (kind << 25) | ref;
+}
 constexpr int kPoolValWords = 3 * 64 + 8;  // k_pool phase B: {L, L cos, L sin} and k0 of 64 entries, 8-B words
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
@@ -150,8 +169,7 @@ struct Ctx {
     uint8_t *valid;
     int32_t *pcur, *pend;  // pooling sweep, per cell: cursor into the cell's run of P, last run position (-1: none)
     // ring of NB per-chunk candidate buffers (chunk ch uses buffer ch % NB):
-    uint64_t *bm_ring;     // candidate bitmap (nwords per buffer)
-    uint32_t *wo_ring;     // candidate index of each bitmap word's first candidate (nwords + 1 per buffer)
+    BmWord *bw_ring;       // candidate bitmap words + first candidate index (nwords per buffer)
     int nblk;              // candidate groups (kGroupCells cells each)
     int64_t cstride;       // candidate slots per buffer: nblk * kGroupCells
     CandHdr *hdr_ring;     // candidates of group g at [g * kGroupCells, ...), ascending cell index
@@ -1452,8 +1470,9 @@ __global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
             acc += (uint32_t)__popcll(bal[i]);
             const int64_t w = g * kChainCells + i;
             if (lane == 0 && w < c.nwords) {
-                c.bm_ring[(int64_t)b * c.nwords + w] = bal[i];
-                c.wo_ring[(int64_t)b * (c.nwords + 1) + w] = woff[i];
+                BmWord *bw = c.bw_ring + (int64_t)b * c.nwords + w;
+                bw->bm = bal[i];
+                bw->wo = woff[i];
             }
         }
 #pragma unroll
@@ -1599,7 +1618,7 @@ __device__ __forceinline__ double wave_max(double v) {
 // segments before r} with the totals at r = nrows.  Returns the flattened
 // length.  LDS private to the calling wave.
 __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_lo, int nrows, int j_lo, int j_hi,
-                                         uint64_t *s_start, int2 *s_row, int2 *s_rinfo) {
+                                         uint64_t *s_start, uint32_t *s_row, int2 *s_rinfo) {
     const int H = c.H;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
     const int WHs = (int)c.WHs;
@@ -1620,8 +1639,7 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
     // All six lookups of both rows are unconditional loads from clamped word
     // indices (a load under a branch would be waited for at the branch end).
     int a0[2], n0[2], a1[2], n1[2];
-    const uint64_t *bmb = c.bm_ring + (int64_t)buf * c.nwords;
-    const uint32_t *wob = c.wo_ring + (int64_t)buf * (c.nwords + 1);
+    const BmWord *bwb = c.bw_ring + (int64_t)buf * c.nwords;
     const int wmax = (int)c.nwords - 1;
     int lo_[2], hi0_[2], hi1_[2], gb_[2];
     bool has_[2], str_[2];
@@ -1645,9 +1663,10 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         hi1_[hh] = l1;
         const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
                   wc = min(max(l1 >> 6, 0), wmax);
-        bA[hh] = bmb[wa]; oA[hh] = wob[wa];
-        bB[hh] = bmb[wb]; oB[hh] = wob[wb];
-        bC[hh] = bmb[wc]; oC[hh] = wob[wc];
+        const BmWord A = bwb[wa], B = bwb[wb], C = bwb[wc];
+        bA[hh] = A.bm; oA[hh] = A.wo;
+        bB[hh] = B.bm; oB[hh] = B.wo;
+        bC[hh] = C.bm; oC[hh] = C.wo;
     }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
@@ -1673,12 +1692,12 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
         if (s_rinfo && r < nrows) s_rinfo[r] = make_int2(start, idx);
         if (n0[hh] > 0) {
-            s_row[idx++] = make_int2(r, a0[hh] - start);
+            s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(a0[hh] - start + kRowBias);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
         if (n1[hh] > 0) {
             const int st1 = start + n0[hh];
-            s_row[idx] = make_int2(r, a1[hh] - st1);
+            s_row[idx] = ((uint32_t)r << 25) | (uint32_t)(a1[hh] - st1 + kRowBias);
             atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
         }
         nz += (int)__popcll(b0) + (int)__popcll(b1);
@@ -1706,9 +1725,9 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
 //   those of the reference given the same local flows.
 template <int K>
 __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                         int row_i0, int f_lo, int f_hi, int m_lo, int jlo, int jhi,
-                                         const uint64_t *s_start, const int2 *s_row, uint2 *s_con, double *s_val,
-                                         uint8_t *s_k0) {
+                                         int row_i0, int f_lo, int f_hi, int m_lo, int jlo, int jhi, int ev0,
+                                         const uint64_t *s_start, const uint32_t *s_row, uint32_t *s_con,
+                                         double *s_val, uint8_t *s_k0) {
     static_assert(3 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
@@ -1739,9 +1758,9 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             const uint64_t mk = s_start[fw >> 6];
             const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
             mbase += (int)__popcll(mk);
-            const int2 rs = s_row[m < 0 ? 0 : m];
-            row = rs.x;
-            k = f + rs.y;
+            const uint32_t rs = s_row[m < 0 ? 0 : m];
+            row = (int)(rs >> 25);
+            k = f + (int)(rs & 0x1FFFFFFu) - kRowBias;
         };
         // software pipeline: the header of step s+1 is in flight while step s
         // is resolved
@@ -1764,7 +1783,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                     const CandVal &cv = cval[kc];
                     const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
                     const FlowCell fe = c.evf[sev];
-                    ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)sev;
+                    ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)(sev - ev0);
                 }
                 if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
                 // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
@@ -1776,14 +1795,14 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                     const int d = di > dj ? di : dj;
                     // smallest scale containing the cell: ceil(d / J)
                     const int k0 = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);
-                    meta = kind | ((uint32_t)k0 << 8);
+                    meta = pack_con(ref, kind, (uint32_t)k0);
                     con = true;
                 }
             }
             const uint64_t bal = __ballot(con);
             if (con) {
                 const int rank = ncon + (int)__popcll(bal & ((1ull << lane) - 1));
-                if (rank >= rank_lo && rank < rank_hi) s_con[rank - rank_lo] = make_uint2(ref, meta);
+                if (rank >= rank_lo && rank < rank_hi) s_con[rank - rank_lo] = meta;
             }
             ncon += (int)__popcll(bal);
             hc = hn; rc = rn; kc = kn;
@@ -1795,10 +1814,10 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     // Address of a staged contributor's {L, L cos, L sin}: the candidate's
     // snapshot (kind 0) or first in-chunk flow (kind 1), or an event's flow
     // (kind 2); every form is three consecutive doubles.
-    auto value_ptr = [&](uint2 en) -> const double * {
-        const uint32_t kind = en.y & 0xFF;
-        const double *pc = reinterpret_cast<const double *>(cval + en.x) + 3 * (kind & 1);
-        const double *pe = reinterpret_cast<const double *>(c.evf + en.x);
+    auto value_ptr = [&](uint32_t en) -> const double * {
+        const uint32_t kind = (en >> 25) & 3u, ref = en & kRefMask;
+        const double *pc = reinterpret_cast<const double *>(cval + ref) + 3 * (kind & 1);
+        const double *pe = reinterpret_cast<const double *>(c.evf + ev0 + ref);
         return kind == 2 ? pe : pc;
     };
     // ---- phase B: the per-scale sums in the reference's order.  vFlow.cpp:998-
@@ -1836,10 +1855,10 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         int wk = K;
         auto fetch = [&](int b0) {
             const int b = b0 + lane;
-            const uint2 en = b < nb ? s_con[b] : make_uint2((uint32_t)e, 2u | ((uint32_t)K << 8));
+            const uint32_t en = b < nb ? s_con[b] : pack_con((uint32_t)(e - ev0), 2u, (uint32_t)K);
             const double *pv = value_ptr(en);
             w0 = pv[0]; w1 = pv[1]; w2 = pv[2];
-            wk = (int)(en.y >> 8);
+            wk = (int)(en >> 27);
         };
         if (nb > 0) fetch(0);
         for (int b0 = 0; b0 < nb; b0 += 64) {
@@ -1910,13 +1929,14 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 // Per-event pooling: the row table of the event's own window, then the event.
 template <int K>
 __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                           uint64_t *s_start, int2 *s_row, uint2 *s_con, double *s_val,
-                                           uint8_t *s_k0) {
+                                           int ev0, uint64_t *s_start, uint32_t *s_row, uint32_t *s_con,
+                                           double *s_val, uint8_t *s_k0) {
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nullptr);
-    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, 0, total, 0, j_lo, j_hi, s_start, s_row, s_con, s_val, s_k0);
+    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, 0, total, 0, j_lo, j_hi, ev0, s_start, s_row, s_con, s_val,
+                s_k0);
 }
 
 // One wavefront per work-order position of [c0, c1) (events of a chunk in
@@ -1946,12 +1966,12 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, i
     if (!vld) return;
     if (ex < c.own_lo || ex >= c.own_hi) return;
     const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap + kPoolValWords);
-    int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
-    uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs);
-    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + kPoolCap);
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap / 2 + kPoolValWords);
+    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
+    uint32_t *s_con = reinterpret_cast<uint32_t *>(s_start + nbw + nrs);
+    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + kPoolCap / 2);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
-    pool_event<K>(c, e, ex, ey, teu, buf, lane, s_start, s_row, s_con, s_val, s_k0);
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_con, s_val, s_k0);
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
@@ -2002,11 +2022,11 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool_grp(Ctx c, int g
     const int i_lo = max(0, xmn - M), i_hi = min(W - 1, xmx + M);
     const int j_lo = max(0, ymn - M), j_hi = min(W - 1, ymx + M);
     const int buf = (ws / c.C2) % c.NB;
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + nri + kPoolCap + kPoolValWords);
-    int2 *s_row = reinterpret_cast<int2 *>(s_start + nbw);
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + nri + kPoolCap / 2 + kPoolValWords);
+    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     int2 *s_rinfo = reinterpret_cast<int2 *>(s_start + nbw + nrs);
-    uint2 *s_con = reinterpret_cast<uint2 *>(s_start + nbw + nrs + nri);
-    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + nri + kPoolCap);
+    uint32_t *s_con = reinterpret_cast<uint32_t *>(s_start + nbw + nrs + nri);
+    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + nri + kPoolCap / 2);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
     pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, s_rinfo);
     for (int w0 = ws; w0 < we; w0 += 64) {
@@ -2027,7 +2047,7 @@ __global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool_grp(Ctx c, int g
             const int r0 = max(xl - M, i_lo) - i_lo, r1 = min(xl + M, i_hi) - i_lo;
             const int2 a = s_rinfo[r0], b = s_rinfo[r1 + 1];
             pool_one<K>(c, el, xl, yl, tl, buf, lane, i_lo, a.x, b.x, a.y, max(0, yl - M), min(W - 1, yl + M),
-                        s_start, s_row, s_con, s_val, s_k0);
+                        (ws / c.C2) * c.C2, s_start, s_row, s_con, s_val, s_k0);
         }
     }
 }
@@ -2181,8 +2201,7 @@ struct farms_handle {
     int32_t *pcur = nullptr, *pend = nullptr;
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1)
     int pool_batch = kDefaultPoolBatch, NB = 2 * kDefaultPoolBatch + 1;
-    uint64_t *bm_ring = nullptr;
-    uint32_t *wo_ring = nullptr;
+    BmWord *bw_ring = nullptr;
     int nblk = 0;
     int64_t cstride = 0;
     CandHdr *hdr_ring = nullptr;
@@ -2324,13 +2343,13 @@ int reset_surfaces(farms_handle *h) {
 template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap + kPoolValWords);
+    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap / 2 + kPoolValWords);
     hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), lds, s, c, c0, c1);
 }
 
 template <int K>
 void launch_pool_grp(const Ctx &c, int g0, int g1, hipStream_t s) {
-    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + c.pool_ri + kPoolCap + kPoolValWords);
+    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + c.pool_ri + kPoolCap / 2 + kPoolValWords);
     if (g1 > g0) hipLaunchKernelGGL(k_pool_grp<K>, dim3(ceil_div(g1 - g0, 4)), dim3(256), lds, s, c, g0, g1);
 }
 
@@ -2428,13 +2447,13 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.pcur = h->pcur; c.pend = h->pend;
     c.tprev = h->prm.serial ? h->tprev : nullptr;
-    c.bm_ring = h->bm_ring; c.wo_ring = h->wo_ring; c.nblk = h->nblk; c.cstride = h->cstride;
+    c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     // a group's union window spans <= 2M + 2^tile_shift rows and columns
     const int span = h->pool_groups ? 2 * h->M + (1 << h->tile_shift) : 2 * h->M + 1;
     c.pool_bw = (span * span + 63) / 64;  // flattened window positions
-    c.pool_rs = 2 * span;                 // <= 2 segments per window row
+    c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
     c.pool_ri = h->pool_groups ? span + 1 : 0;
     c.gstart = h->gstart;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
@@ -2675,8 +2694,8 @@ extern "C" int farms_default_params(farms_params *o) {
 extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (!prm || !out) return fail(FARMS_EINVAL, "null argument");
     *out = nullptr;
-    if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height >= (int64_t(1) << 29))
-        return fail(FARMS_EINVAL, "sensor size out of range");
+    if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height > kMaxSlots)
+        return fail(FARMS_EINVAL, "sensor size out of range (at most 2^24 - 256 pixels)");
     if (prm->window_jump <= 0 || prm->max_window < 0) return fail(FARMS_EINVAL, "bad pooling scales");
     if (prm->region_width < 0 || (prm->region_width > 0 && (prm->region_x0 < 0 || prm->region_x0 + prm->region_width > prm->width)))
         return fail(FARMS_EINVAL, "stored region outside the sensor");
@@ -2718,6 +2737,10 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;
     if (prm->pool_batch > 0) h->pool_batch = prm->pool_batch;
+    if (h->pool_chunk > (1 << 24)) {
+        delete h;
+        return fail(FARMS_EINVAL, "pool_chunk above 2^24");
+    }
     h->NB = 2 * h->pool_batch + 1;
     h->nwords = (h->WH + 63) / 64;
     h->nblk = (int)((h->WH + kGroupCells - 1) / kGroupCells);
@@ -2751,8 +2774,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->pcur, h->WH)) || (rc = dalloc(&h->pend, h->WH)) ||
-        (rc = dalloc(&h->bm_ring, h->nwords * h->NB)) || 
-        (rc = dalloc(&h->wo_ring, (h->nwords + 1) * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
+        (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
         (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
@@ -2767,7 +2789,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     free_workspace(h);
     dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
-    dfree(h->pcur); dfree(h->pend); dfree(h->bm_ring); dfree(h->wo_ring);
+    dfree(h->pcur); dfree(h->pend); dfree(h->bw_ring);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);

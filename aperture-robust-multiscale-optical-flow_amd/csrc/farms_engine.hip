@@ -49,6 +49,20 @@
 #include "../../include/farms_hip.h"
 #include "farms_libm.h"
 
+// FARMS_OCML_LIBM=1: ROCm's faithful (not correctly rounded) atan2/sin/cos
+// instead of farms_libm.h -- A/B aid only, breaks bitwise parity
+#if defined(FARMS_OCML_LIBM) && FARMS_OCML_LIBM
+#define F_ATAN2 ::atan2
+#define F_COS ::cos
+#define F_SIN ::sin
+#define F_SINCOS ::sincos
+#else
+#define F_ATAN2 farms_libm::cr_atan2
+#define F_COS farms_libm::cr_cos
+#define F_SIN farms_libm::cr_sin
+#define F_SINCOS farms_libm::cr_sincos
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -550,9 +564,11 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = farms_libm::cr_atan2(r0, r1);
-    vx_out = speed * farms_libm::cr_cos(angle);
-    vy_out = speed * farms_libm::cr_sin(angle);
+    const double angle = F_ATAN2(r0, r1);
+    double sn_, cs_;
+    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+    vx_out = speed * cs_;
+    vy_out = speed * sn_;
 }
 
 // Local plane fit of one event with fRad known at compile time (the common
@@ -725,9 +741,11 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = farms_libm::cr_atan2(r0, r1);
-    vx_out = speed * farms_libm::cr_cos(angle);
-    vy_out = speed * farms_libm::cr_sin(angle);
+    const double angle = F_ATAN2(r0, r1);
+    double sn_, cs_;
+    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+    vx_out = speed * cs_;
+    vy_out = speed * sn_;
 }
 
 // Validity gate, flow-surface value and record of one fitted event.
@@ -742,10 +760,12 @@ __device__ __forceinline__ void fit_store(const Ctx &c, int e, double vx, double
     double L = 0.0, th = 0.0;
     if (ok) {
         L = sqrt(vx * vx + vy * vy);
-        th = farms_libm::cr_atan2(vy, vx);
+        th = F_ATAN2(vy, vx);
         f.L = L;
-        f.Lc = L * farms_libm::cr_cos(th);
-        f.Ls = L * farms_libm::cr_sin(th);
+        double sn_, cs_;
+        F_SINCOS(th, &sn_, &cs_);
+        f.Lc = L * cs_;
+        f.Ls = L * sn_;
     } else {
         f.L = 0.0; f.Lc = 0.0; f.Ls = 0.0;
     }
@@ -820,6 +840,11 @@ __device__ __forceinline__ uint64_t quad_or_u64(uint64_t v) {
     return v | ((uint64_t)(uint32_t)xch32<1>(hi) << 32) | (uint32_t)xch32<1>(lo);
 }
 
+#ifndef FARMS_FIT_WPB
+#define FARMS_FIT_WPB 1  // waves per k_fit_quad workgroup (16 events each)
+#endif
+constexpr int kFitQS = 16 * FARMS_FIT_WPB;  // quads per fit workgroup: stride of the LDS stamp tiles
+
 template <int FR>
 __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq, int j, uint32_t *lt, double &vx_out,
                                                double &vy_out) {
@@ -893,7 +918,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
 
     // ---- gather the winning window, cx-major (vFlow.cpp:923-930): this lane's
-    // columns into LDS (lt[k * 64]), visited mask combined over the quad
+    // columns into LDS (lt[k * kFitQS]), visited mask combined over the quad
     const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
     uint64_t vis = 0;
 #pragma unroll 1
@@ -906,7 +931,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
             const int k = cxo * side + cyo;
             const int64_t st = sae_resolve_h(c, col[cyo], (uint32_t)((u - c.X0) * H + bj - FR + cyo), e, seq);
             vis |= st >= 0 ? 1ull << k : 0ull;
-            lt[k * 64] = st < 0 ? 0u : (uint32_t)st;
+            lt[k * kFitQS] = st < 0 ? 0u : (uint32_t)st;
         }
     }
     vis = quad_or_u64(vis);
@@ -916,7 +941,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
         const int cx = bi + k / side - FR, cy = bj + k % side - FR;
         const bool vk = (vis >> k) & 1;
-        X = vk ? cx : 0; Y = vk ? cy : 0; T = lt[k * 64];
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = lt[k * kFitQS];
     };
     int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
 #pragma unroll 1
@@ -982,13 +1007,15 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = farms_libm::cr_atan2(r0, r1);
-    vx_out = speed * farms_libm::cr_cos(angle);
-    vy_out = speed * farms_libm::cr_sin(angle);
+    const double angle = F_ATAN2(r0, r1);
+    double sn_, cs_;
+    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+    vx_out = speed * cs_;
+    vy_out = speed * sn_;
 }
 
 // Variant that keeps the union: every lane writes the stamps of its union
-// columns to the wave's LDS tile (ut[cell * 64], cell = column * US + row) and
+// columns to the wave's LDS tile (ut[cell * kFitQS], cell = column * US + row) and
 // their visited bits to a register mask, so the winning window needs no second
 // round of loads (window column cxo is union column (bw / 3) * FR + cxo).
 template <int FR>
@@ -1044,7 +1071,7 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
             if (v < 0 || v >= H) continue;
             const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
             const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-            ut[(ucol * US + i) * 64] = tk;
+            ut[(ucol * US + i) * kFitQS] = tk;
             umask |= st >= 0 ? 1ull << ((ucol >> 2) * US + i) : 0ull;
             dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
         }
@@ -1090,7 +1117,7 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
         const int kx = k / side, ky = k % side;
         const int cx = bi + kx - FR, cy = bj + ky - FR;
         const bool vk = (vis >> k) & 1;
-        X = vk ? cx : 0; Y = vk ? cy : 0; T = ut[((ub + kx) * US + vb + ky) * 64];
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = ut[((ub + kx) * US + vb + ky) * kFitQS];
     };
     int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
 #pragma unroll 1
@@ -1156,9 +1183,11 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
     const double speed = 1.0 / dtdp;
-    const double angle = farms_libm::cr_atan2(r0, r1);
-    vx_out = speed * farms_libm::cr_cos(angle);
-    vy_out = speed * farms_libm::cr_sin(angle);
+    const double angle = F_ATAN2(r0, r1);
+    double sn_, cs_;
+    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+    vx_out = speed * cs_;
+    vy_out = speed * sn_;
 }
 
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
@@ -1166,9 +1195,9 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
 #define FARMS_FIT_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
 template <int FR, bool UT>
-__global__ __launch_bounds__(256, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
+__global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
-    __shared__ uint32_t s_tk[NPC * 64];
+    __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
     // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
 #ifndef FARMS_FIT_XCD
@@ -1338,9 +1367,11 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
         }
         inliers = (int)wave_sum_i64(inl);
         const double speed = 1.0 / dtdp;
-        const double angle = farms_libm::cr_atan2(r0, r1);
-        dtdx = speed * farms_libm::cr_cos(angle);
-        dtdy = speed * farms_libm::cr_sin(angle);
+        const double angle = F_ATAN2(r0, r1);
+        double sn_, cs_;
+        F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+        dtdx = speed * cs_;
+        dtdy = speed * sn_;
     }
     if (lane == 0) {
         double vx = 0.0, vy = 0.0;
@@ -1945,15 +1976,18 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #ifndef FARMS_POOL_WAVES
 #define FARMS_POOL_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
+#ifndef FARMS_POOL_WPB
+#define FARMS_POOL_WPB 1  // waves (events) per k_pool workgroup: one, so that a finished event frees its slot at once
+#endif
 template <int K>
-__global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
+__global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
     // LDS per wave, sized for maxWindow M at launch (pool_lds_bytes): segment-
     // start bitmap over the flattened window, <= 2 row segments per window
     // row, kPoolCap staged contributors, the values and k0 of 64 of them
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int w = c0 + work_block() * 4 + wv;
+    const int w = c0 + work_block() * FARMS_POOL_WPB + wv;
     if (w >= c1) return;
     const int e = c.Q[w];
     // the event's fields load together with its validity flag
@@ -2061,7 +2095,7 @@ __global__ void k_true_polar(Ctx c, int e0, int e1) {
     if (x < c.own_lo || x >= c.own_hi) return;
     const double gx = c.r_true[e], gy = c.th_true[e];
     c.r_true[e] = sqrt(gy * gy + gx * gx);
-    c.th_true[e] = farms_libm::cr_atan2(gy, gx);
+    c.th_true[e] = F_ATAN2(gy, gx);
 }
 
 // ---------------------------------------------------------------------------
@@ -2343,8 +2377,8 @@ int reset_surfaces(farms_handle *h) {
 template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap / 2 + kPoolValWords);
-    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, 4)), dim3(256), lds, s, c, c0, c1);
+    const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap / 2 + kPoolValWords);
+    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, FARMS_POOL_WPB)), dim3(64 * FARMS_POOL_WPB), lds, s, c, c0, c1);
 }
 
 template <int K>
@@ -2379,7 +2413,7 @@ pool_launcher pool_for(int K) {
 
 void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile) {
     if (quad) {
-        const dim3 g(ceil_div(c1 - c0, 64)), b(256);
+        const dim3 g(ceil_div(c1 - c0, kFitQS)), b(64 * FARMS_FIT_WPB);
         switch (fr) {
         case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq); return;
         case 2:
@@ -3074,6 +3108,16 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
 
+    // one completion event per pooling super-chunk, created before the worker
+    // threads start: the hook must not grow copy_ev while they read it
+    {
+        const int64_t n_super = ceil_div(ceil_div(n, h->pool_chunk), h->pool_batch);
+        while ((int64_t)h->copy_ev.size() < n_super) {
+            hipEvent_t ev;
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            h->copy_ev.push_back(ev);
+        }
+    }
     struct Ready { int S, p0, p1; };
     std::mutex mu;
     std::condition_variable cv;
@@ -3113,11 +3157,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         return code;
     };
     super_hook hook = [&](int S, int p0, int p1, hipEvent_t done) -> int {
-        while ((int)h->copy_ev.size() <= S) {
-            hipEvent_t ev;
-            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            h->copy_ev.push_back(ev);
-        }
+        if ((int)h->copy_ev.size() <= S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
         HIPCHK(hipStreamWaitEvent(h->s_copy, done, 0));
         const size_t k = (size_t)(p1 - p0);
         for (int c = 0; c < 6; ++c)

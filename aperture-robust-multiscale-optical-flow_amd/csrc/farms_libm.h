@@ -229,7 +229,7 @@ __host__ __device__ inline double sin_quadrant(dd r, int q) {
     return (q & 2) ? -v.hi : v.hi;  // v.hi = RN(v.hi + v.lo): the normalised sum
 }
 
-__host__ __device__ inline double cr_sin(double x) {
+__host__ __device__ inline double sin_dd(double x) {
     const double ax = __builtin_fabs(x);
     if (!(ax < 67108864.0)) return x - x + __builtin_nan("");  // NaN, inf, |x| >= 2^26: outside the domain
     if (ax < 0x1p-30) return x;              // sin x = x (1 - x^2/6): within half an ulp of x
@@ -238,7 +238,7 @@ __host__ __device__ inline double cr_sin(double x) {
     return sin_quadrant(r, q);
 }
 
-__host__ __device__ inline double cr_cos(double x) {
+__host__ __device__ inline double cos_dd(double x) {
     const double ax = __builtin_fabs(x);
     if (!(ax < 67108864.0)) return x - x + __builtin_nan("");
     if (ax < 0x1p-30) return 1.0;  // cos x = 1 - x^2/2: within half an ulp of 1
@@ -262,7 +262,7 @@ __host__ __device__ inline dd atan_01(dd t) {
     return dd_add(dd_c(kAtanTab[j]), dd_mul(s, u));
 }
 
-__host__ __device__ inline double cr_atan2(double y, double x) {
+__host__ __device__ inline double atan2_dd(double y, double x) {
     if (x != x || y != y) return x + y;
     const bool xneg = __builtin_signbit(x);
     const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
@@ -284,6 +284,107 @@ __host__ __device__ inline double cr_atan2(double y, double x) {
         res = a.hi;
     }
     return __builtin_copysign(res, y);
+}
+
+// ---- fast paths (Ziv): a cheaper evaluation with a proven error bound, and
+// its result only where that bound decides the rounding; elsewhere (about one
+// call in 2^12) the full double-double evaluation above.  Both round correctly,
+// so the functions below return exactly what sin_dd / cos_dd / atan2_dd do.
+//
+// round_ok: v = hi + lo (normalised) approximates the true value t with
+// |t - v| < eps * |hi|; RN(t) = hi iff both ends of that interval round to hi
+// (rounding is monotone).  kFastEps leaves a factor >= 8 over the evaluation
+// errors derived below.
+constexpr double kFastEps = 0x1p-66;
+#ifndef FARMS_LIBM_FALLBACK
+#define FARMS_LIBM_FALLBACK() ((void)0)  // host check builds count the full evaluations here
+#endif
+__host__ __device__ inline bool round_ok(dd v) {
+    const double e = kFastEps * __builtin_fabs(v.hi);
+    return v.hi + (v.lo + e) == v.hi && v.hi + (v.lo - e) == v.hi;
+}
+// sin(r) = r (1 + u) and cos(r) = 1 + u' on |r| <= pi/4 + 2^-50, z = r^2 <= 0.62:
+// the Taylor terms n >= 4 in double (Horner on z.hi; truncation after n = 9
+// below z^10 / 21! < 2^-72 relative; rounding < 2^-69 of the result, these
+// terms being < 2.2e-6 / 2.5e-5 of it), n = 1..3 in double-double.
+__host__ __device__ inline dd sin_poly_fast(dd r, dd z) {
+    double t = kSinC[9][0];
+    for (int n = 8; n >= 4; --n) t = __builtin_fma(t, z.hi, kSinC[n][0]);
+    dd a = dd_add_d(dd_c(kSinC[3]), t * z.hi);             // S3 + z T
+    a = dd_add(dd_c(kSinC[2]), dd_mul(a, z));              // S2 + z a
+    a = dd_add(dd_c(kSinC[1]), dd_mul(a, z));              // S1 + z a
+    return dd_add(r, dd_mul(r, dd_mul(a, z)));             // r + r z a
+}
+__host__ __device__ inline dd cos_poly_fast(dd z) {
+    double t = kCosC[10][0];
+    for (int n = 9; n >= 4; --n) t = __builtin_fma(t, z.hi, kCosC[n][0]);
+    dd a = dd_add_d(dd_c(kCosC[3]), t * z.hi);
+    a = dd_add(dd_c(kCosC[2]), dd_mul(a, z));
+    a = dd_add(dd_c(kCosC[1]), dd_mul(a, z));
+    return dd_add_d(dd_mul(a, z), 1.0);                    // 1 + z a
+}
+// sin and cos of x (|x| < 2^26), correctly rounded, one range reduction
+__host__ __device__ inline void cr_sincos(double x, double *s, double *c) {
+    const double ax = __builtin_fabs(x);
+    if (!(ax < 67108864.0)) { *s = *c = x - x + __builtin_nan(""); return; }
+    if (ax < 0x1p-30) { *s = x; *c = 1.0; return; }
+    int q;
+    const dd r = reduce_pio2(x, q);
+    dd z = two_prod(r.hi, r.hi);
+    z.lo += 2.0 * r.hi * r.lo;
+    z = fast_two_sum(z.hi, z.lo);
+    const dd ps = sin_poly_fast(r, z), pc = cos_poly_fast(z);
+    // quadrant q: sin x = (+-) sin r or cos r, cos x likewise one quadrant on
+    const dd vs = (q & 1) ? pc : ps, vc = (q & 1) ? ps : pc;
+    const bool ok = round_ok(vs) && round_ok(vc);
+    double sv = (q & 2) ? -vs.hi : vs.hi;
+    double cv = ((q + 1) & 2) ? -vc.hi : vc.hi;
+    if (!ok) { FARMS_LIBM_FALLBACK(); sv = sin_dd(x); cv = cos_dd(x); }
+    *s = sv;
+    *c = cv;
+}
+__host__ __device__ inline double cr_sin(double x) {
+    double s, c;
+    cr_sincos(x, &s, &c);
+    return s;
+}
+__host__ __device__ inline double cr_cos(double x) {
+    double s, c;
+    cr_sincos(x, &s, &c);
+    return c;
+}
+// atan2 for finite nonzero x, y with min/max >= 2^-960 (t and its remainder
+// stay normal): atan(t) = atan(c) + atan(u), u = (t - c) / (1 + t c), |u| <=
+// 2^-7 + 2^-50, u to ~2^-100 (two quotient digits); atan(u) = u (1 + w), w =
+// -u^2/3 in double-double plus the terms u^4..u^8 in double (< 2^-30: rounding
+// below 2^-80; truncation u^10 / 11 < 2^-73), atan(c) from the table.
+__host__ __device__ inline double cr_atan2(double y, double x) {
+    const double ax = __builtin_fabs(x), ay = __builtin_fabs(y);
+    const bool swap = ay > ax;
+    const double n = swap ? ax : ay, d = swap ? ay : ax;
+    // NaN, zero, infinite or badly scaled operands: the full evaluation
+    if (!(n > 0.0) || !(d < __builtin_inf()) || !(n >= 0x1p-960 * d)) return atan2_dd(y, x);
+    const double qh = n / d;
+    const dd t = fast_two_sum(qh, __builtin_fma(-qh, d, n) / d);
+    const int j = (int)__builtin_rint(t.hi * 64.0);
+    const double cj = (double)j * 0.015625;
+    const dd num = fast_two_sum(t.hi - cj, t.lo);          // t.hi - cj exact (Sterbenz; cj = 0 trivially)
+    const dd den = dd_add_d(dd_mul_d(t, cj), 1.0);         // 1 + t c
+    const double q1 = num.hi / den.hi;
+    const dd rem = dd_add(num, dd_neg(dd_mul_d(den, q1)));
+    const dd u = fast_two_sum(q1, rem.hi / den.hi);
+    dd z = two_prod(u.hi, u.hi);
+    z.lo += 2.0 * u.hi * u.lo;
+    double tail = __builtin_fma(z.hi, kAtanC[4][0], kAtanC[3][0]);
+    tail = __builtin_fma(z.hi, tail, kAtanC[2][0]);
+    tail *= z.hi * z.hi;
+    const dd w = dd_add_d(dd_mul(z, dd_c(kAtanC[1])), tail);
+    const dd au = dd_add(u, dd_mul(u, w));
+    dd a = dd_add(dd_c(kAtanTab[j]), au);
+    if (swap) a = dd_add(dd{kPio2_hi, kPio2_lo}, dd_neg(a));
+    if (__builtin_signbit(x)) a = dd_add(dd{kPi_hi, kPi_lo}, dd_neg(a));
+    if (!round_ok(a)) { FARMS_LIBM_FALLBACK(); return atan2_dd(y, x); }
+    return __builtin_copysign(a.hi, y);
 }
 
 }  // namespace farms_libm

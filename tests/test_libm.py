@@ -22,6 +22,8 @@ def lib():
     lib = ctypes.CDLL(LIB)
     lib.farms_libm_check.restype = ctypes.c_int64
     lib.farms_libm_check.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int64] + [ctypes.c_void_p] * 2
+    lib.farms_libm_fast_check.restype = ctypes.c_int64
+    lib.farms_libm_fast_check.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int64, ctypes.c_void_p]
     return lib
 
 
@@ -92,3 +94,22 @@ def test_glibc_misrounding_rate(lib):
         assert cr[i] == float(mpmath.atan2(mpmath.mpf(float(y[i])), mpmath.mpf(float(x[i]))))
     print("glibc misrounding rates:", rates)
     assert all(r < 0.005 for r in rates.values()), rates
+
+
+def test_fast_path_equals_full_evaluation(lib):
+    """The Ziv fast paths (farms_libm.h: cheaper evaluation + rounding test,
+    full double-double evaluation where the test cannot decide) return bitwise
+    what the full evaluation alone returns, and fall back rarely (~2^-11)."""
+    rng = np.random.default_rng(11)
+    n = 1_000_000
+    ang, y, x = samples(rng, n)
+    k = rng.integers(-4, 5, n // 4)
+    edge = k * (np.pi / 4) + rng.standard_normal(n // 4) * 10.0 ** rng.uniform(-16, -1, n // 4)
+    fb = ctypes.c_int64(0)
+    for fn, a, b in ((1, ang, ang), (2, ang, ang), (1, edge, edge), (2, edge, edge), (0, y, x),
+                     (0, np.tan(ang), np.ones(n))):
+        a = np.ascontiguousarray(a, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        diff = lib.farms_libm_fast_check(fn, a.ctypes.data, b.ctypes.data, a.size, ctypes.byref(fb))
+        assert diff == 0, (fn, diff)
+        assert fb.value / a.size < 1e-3, (fn, fb.value)

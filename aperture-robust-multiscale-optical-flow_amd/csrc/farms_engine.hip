@@ -142,19 +142,12 @@ struct CandVal {
 };
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
-constexpr int kPoolCap = 256;  // contributors staged in LDS per wave and pass
-// LDS packing of k_pool's row segments and staged contributors (32 bits each):
-//   row segment  = row << 25 | (candidate index - flattened index + kRowBias)
-//   contributor  = k0 << 27 | kind << 25 | ref (kinds 0/1: candidate index;
-//                  kind 2: event id - the chunk's first event id)
-// valid while candidate slots (and pooling chunks) stay below 2^24
+// LDS packing of k_pool's row segments (32 bits each):
+//   row segment = row << 25 | (candidate index - flattened index + kRowBias)
+// valid while candidate slots stay below 2^24 (W * H <= kMaxSlots)
 constexpr int kRowBias = 1 << 14;  // flattened positions of a window < 128 x 128
-constexpr uint32_t kRefMask = (1u << 25) - 1;
 constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
-__device__ __forceinline__ uint32_t pack_con(uint32_t ref, uint32_t kind, uint32_t k0) {
-    return (k0 << 27) | (kind << 25) | ref;
-}
-constexpr int kPoolValWords = 3 * 64 + 8;  // k_pool phase B: {L, L cos, L sin} and k0 of 64 entries, 8-B words
+constexpr int kPoolValWords = 3 * 64 + 8;  // k_pool staging: {L, L cos, L sin} and k0 of 64 entries, 8-B words
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -191,8 +184,6 @@ struct Ctx {
     int64_t nwords;
     int NB, C2;            // ring size, events per pooling chunk
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
-    int pool_ri;           // k_pool_grp: row-info words (rows + 1)
-    const int32_t *gstart; // pooling groups: first work-order position of group g (gstart[G] = n)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): per event, the stamp
     // its pixel's lastEventTime holds while the event is pooled (written only
@@ -343,36 +334,28 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
     }
 }
 
-// Pooling groups (k_pool_grp): a group starts where the (pooling chunk, tile)
-// key of the work order changes, and at every split-th position inside a run.
-__global__ void k_group_flags(const uint32_t *wkey_sorted, int n, int split, uint8_t *flags) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= n) return;
-    flags[w] = (w == 0 || wkey_sorted[w] != wkey_sorted[w - 1] || w % split == 0) ? 1 : 0;
-}
-
-// gstart[G] = n; chunk_g0[ch] = first group of pooling chunk ch (chunk ch
-// holds work-order positions [ch * C2, (ch + 1) * C2): every chunk has groups),
-// chunk_g0[nch] = G.
-__global__ void k_group_index(int n, const int *ng, int32_t *gstart, int C2, int32_t *chunk_g0, int nch) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int G = *ng;
-    if (g >= G) return;
-    const int ch = gstart[g] / C2;
-    if (g == 0 || gstart[g - 1] / C2 != ch) chunk_g0[ch] = g;
-    if (g == 0) {
-        gstart[G] = n;
-        chunk_g0[nch] = G;
-    }
-}
-
 // Fit sweep, between chunks (one launch): for chunk f = [c0, c1), record at
 // every touched pixel its first two in-chunk events inline and the bounds of
 // its in-chunk run in P, and set the SAE snapshot to the pixel's last event
 // before the chunk (prev of its first event); for chunk f-1 = [p0, c0), set
 // the snapshot of pixels it touched that chunk f does not touch.  The two
 // parts write disjoint cells.
+// Wave priority of the fit sweep's kernels: each fit launch waits for its
+// predecessor's slowest wave, and those waves share their SIMDs with the
+// pooling waves of the stream beside it; raising their issue priority keeps
+// the fit chain from stretching (FARMS_FIT_PRIO 0 = none).
+#ifndef FARMS_FIT_PRIO
+#define FARMS_FIT_PRIO 0
+#endif
+__device__ __forceinline__ void fit_prio() {
+    if (FARMS_FIT_PRIO) __builtin_amdgcn_s_setprio(FARMS_FIT_PRIO);
+}
+#ifndef FARMS_CHAIN_PRIO
+#define FARMS_CHAIN_PRIO 0
+#endif
+
 __global__ void k_fit_prep(Ctx c, int p0, int c0, int c1, uint32_t seq) {
+    fit_prio();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int ep = p0 + i;
     if (ep < c0) {
@@ -1196,6 +1179,7 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
 #endif
 template <int FR, bool UT>
 __global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
+    fit_prio();
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
@@ -1437,6 +1421,7 @@ __device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
     return ChainFlow{f.L, f.Lc, f.Ls, f.t};
 }
 __global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
+    if (FARMS_CHAIN_PRIO) __builtin_amdgcn_s_setprio(FARMS_CHAIN_PRIO);
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= c.nblk) return;
@@ -1617,24 +1602,15 @@ __device__ __forceinline__ double wave_max(double v) {
 //   with j clipped to W-1 as the reference does (vFlow.cpp:1000/1113): for W > H
 //   a row runs into the next column (aliasing kept); indices >= W*H do not
 //   contribute.  Each row is a contiguous slice of the chunk's candidate list
-//   (bitmap popcount prefix); the slices are flattened.
-//   Phase A: lanes scan the flattened candidates 64 at a time (coalesced 16-B
-//   headers), resolve each cell's state as of e, and compact the contributors
-//   (valid flow, |dt| < 500 us) into LDS in ascending cell order (ballot).
-//   Phase B: lane g*K + k sums quantity g (L, L cos, L sin) of scale k over the
-//   staged list sequentially, in the reference's raster order (vFlow.cpp:998-
-//   1021): the per-scale sums, means and the first strict maximum are bitwise
-//   those of the reference given the same local flows.
+//   (bitmap popcount prefix); the slices are flattened (pool_rows).
+//   Then one pass over the flattened candidates, 64 per step, in raster order:
+//   resolve each cell's state as of e, load the values of the contributors
+//   (valid flow, |dt| < 500 us), stage them in LDS in rank order (ballot) and
+//   fold them into the per-scale sums in the reference's order (pool_one).
 // The summation order depends only on the contributor list, so results are
 // bitwise independent of chunking and streaming splits.
-// Pooling of one valid owned event e at (ex, ey, teu) by the calling wave,
-// against candidate buffer buf.  LDS (private to the wave): s_start bit f set
-// iff a non-empty row segment starts at flattened candidate position f;
-// s_row the non-empty segments in order {row, candidate index - flattened
-// index}; s_con the staged contributors {ref, kind | k0 << 8}; s_val / s_k0
-// the values {L, L cos, L sin} and k0 of 64 staged entries.
 #ifndef FARMS_POOL_STOP
-#define FARMS_POOL_STOP 0  // ablation aid (variants only): 1 row setup, 2 + phase A, 3 all but the phase B folds
+#define FARMS_POOL_STOP 0  // ablation aid (variants only): 1 row setup only, 3 all but the folds
 #endif
 #ifndef FARMS_POOL_UNROLL
 #define FARMS_POOL_UNROLL 8  // phase B entries per loop trip (4 or 8; 64 must be a multiple)
@@ -1645,11 +1621,9 @@ __device__ __forceinline__ double wave_max(double v) {
 // row runs into the next column; indices >= W*H do not contribute).  Writes
 // s_start (bit f set iff a non-empty row segment starts at flattened position
 // f), s_row (the non-empty segments in order: {row, candidate index - flattened
-// index}) and, when s_rinfo is given, per row r {flattened start, non-empty
-// segments before r} with the totals at r = nrows.  Returns the flattened
-// length.  LDS private to the calling wave.
+// index}).  Returns the flattened length.  LDS private to the calling wave.
 __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_lo, int nrows, int j_lo, int j_hi,
-                                         uint64_t *s_start, uint32_t *s_row, int2 *s_rinfo) {
+                                         uint64_t *s_start, uint32_t *s_row) {
     const int H = c.H;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;  // local cell = global cell - OFF
     const int WHs = (int)c.WHs;
@@ -1721,7 +1695,6 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         const uint64_t lt = (1ull << lane) - 1;
         const uint64_t b0 = __ballot(n0[hh] > 0), b1 = __ballot(n1[hh] > 0);
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
-        if (s_rinfo && r < nrows) s_rinfo[r] = make_int2(start, idx);
         if (n0[hh] > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(a0[hh] - start + kRowBias);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
@@ -1734,7 +1707,6 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         nz += (int)__popcll(b0) + (int)__popcll(b1);
         carry += __builtin_amdgcn_readlane(incl, 63);
     }
-    if (s_rinfo && lane == 0) s_rinfo[nrows] = make_int2(carry, nz);
     // the LDS arrays are private to this wave: a wavefront-scope fence orders
     // the writes above before the reads below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1743,22 +1715,29 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
 }
 
 // Pooling of one valid owned event e at (ex, ey, teu) by the calling wave from
-// a row table built by pool_rows (rows from absolute row row_i0): the
-// flattened candidates [f_lo, f_hi) cover the event's window rows, m_lo
-// non-empty segments start before f_lo, and cells outside j in [jlo, jhi] are
-// not in its window (a group's union table is wider than one event's window).
-//   Phase A: lanes scan the candidates 64 at a time (coalesced 16-B headers,
-//   one step ahead in flight), resolve each cell's state as of e, and compact
-//   the contributors (valid flow, |dt| < 500 us) into LDS in raster order.
-//   Phase B: lane g*K + k sums quantity g (L, L cos, L sin) of scale k over the
-//   staged list sequentially, in the reference's raster order (vFlow.cpp:998-
-//   1021): the per-scale sums, means and the first strict maximum are bitwise
-//   those of the reference given the same local flows.
+// the row table built by pool_rows (rows from absolute row row_i0): flattened
+// candidates [0, total).  One pass, 64 candidates per step, software-pipelined:
+//   step s resolves the headers of s (loaded during step s-1: the cell's state
+//   as of e -- snapshot, first in-chunk flow, or a run search when the cell
+//   fired more than once in the chunk), keeps the contributors (valid flow,
+//   |t_e - t_cell| < 500 us, vFlow.cpp:1002/1115) and issues the loads of
+//   their values {L, L cos, L sin} and of the headers of s+1; meanwhile the
+//   contributors of s-1 (values landed) go to LDS in rank order and are folded.
+//   Fold: lane g*K + kk adds entry after entry to its sum of quantity g (L,
+//   L cos, L sin) of scale kk, members only (k0 <= kk): vFlow.cpp:998-1021
+//   accumulates each scale from 0, cell by cell, i ascending then j ascending,
+//   and the staged entries are exactly the contributors of the largest window
+//   in that order (row slices in row order, ascending cells within a row; a
+//   cell the W-1 clip aliases into two rows appears twice, as the reference
+//   visits it twice).  So every per-scale sum, mean and the first strict
+//   maximum are bitwise the reference's given the same local flows.  Counts
+//   per scale are integers (ballots, any order).
+// LDS (private to the wave): s_val / s_k0 the values and k0 of one step's
+// 64 staged entries (contributors first, in rank order).
 template <int K>
 __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                         int row_i0, int f_lo, int f_hi, int m_lo, int jlo, int jhi, int ev0,
-                                         const uint64_t *s_start, const uint32_t *s_row, uint32_t *s_con,
-                                         double *s_val, uint8_t *s_k0) {
+                                         int row_i0, int total, int ev0, const uint64_t *s_start,
+                                         const uint32_t *s_row, double *s_val, uint8_t *s_k0) {
     static_assert(3 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
@@ -1768,142 +1747,93 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     // holds (the previous event's), not the event's own (vFlow.cpp:790 vs :264)
     const uint32_t own_lin = c.tprev ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
     const uint32_t own_tprev = c.tprev ? c.tprev[e] : 0u;
-    const int total = f_hi - f_lo;
+    (void)ev0;
 #if FARMS_POOL_STOP == 1
     if (lane == 0) c.scale[e] = total;  // ablation: row setup only
     return;
 #endif
-
-    // ---- phase A: stage contributors with rank in [pass*cap, (pass+1)*cap) in
-    // LDS; returns the total number of contributors
-    auto collect = [&](int pass) -> int {
-        const int rank_lo = pass * kPoolCap, rank_hi = rank_lo + kPoolCap;
-        int ncon = 0;
-        // Flattened positions [fw, fw + 64) (fw a multiple of 64, steps in
-        // order): lane f's segment is the last non-empty one starting at or
-        // before f, i.e. the (number of segment starts <= f)-th one.
-        const int fw0 = f_lo & ~63;
-        // non-empty segments starting before fw: m_lo less those in [fw0, f_lo)
-        int mbase = m_lo - (int)__popcll(s_start[fw0 >> 6] & ((1ull << (f_lo & 63)) - 1));
-        auto locate = [&](int fw, int f, int &row, int &k) {
-            const uint64_t mk = s_start[fw >> 6];
-            const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
-            mbase += (int)__popcll(mk);
-            const uint32_t rs = s_row[m < 0 ? 0 : m];
-            row = (int)(rs >> 25);
-            k = f + (int)(rs & 0x1FFFFFFu) - kRowBias;
-        };
-        // software pipeline: the header of step s+1 is in flight while step s
-        // is resolved
-        int rc = 0, kc = 0;
-        CandHdr hc{};
-        if (f_hi > f_lo) { locate(fw0, fw0 + lane, rc, kc); if (fw0 + lane >= f_lo && fw0 + lane < f_hi) hc = chdr[kc]; }
-        for (int f0 = fw0; f0 < f_hi; f0 += 64) {
-            const int f = f0 + lane, fn = f + 64;
-            int rn = 0, kn = 0;
-            CandHdr hn{};
-            if (f0 + 64 < f_hi) { locate(f0 + 64, fn, rn, kn); if (fn < f_hi) hn = chdr[kn]; }
-            bool con = false;
-            uint32_t ref = 0, meta = 0;
-            if (f >= f_lo && f < f_hi) {
-                uint32_t tq, kind;
-                bool ok;
-                if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; kind = 0; ref = (uint32_t)kc; }
-                else if (!(hc.lin & kCandMore)) { ok = (hc.lin & kCandOneOk) != 0; tq = hc.t1; kind = 1; ref = (uint32_t)kc; }
-                else {  // several events at the cell inside the chunk: search its run
-                    const CandVal &cv = cval[kc];
-                    const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
-                    const FlowCell fe = c.evf[sev];
-                    ok = fe.L > 0; tq = fe.t; kind = 2; ref = (uint32_t)(sev - ev0);
-                }
-                if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
-                // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
-                const int64_t dt = (int64_t)teu - (int64_t)tq;
-                const int i = row_i0 + rc;
-                const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
-                if (ok && (uint64_t)(dt + 499) < 999u && j >= jlo && j <= jhi) {
-                    const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
-                    const int d = di > dj ? di : dj;
-                    // smallest scale containing the cell: ceil(d / J)
-                    const int k0 = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);
-                    meta = pack_con(ref, kind, (uint32_t)k0);
-                    con = true;
-                }
-            }
-            const uint64_t bal = __ballot(con);
-            if (con) {
-                const int rank = ncon + (int)__popcll(bal & ((1ull << lane) - 1));
-                if (rank >= rank_lo && rank < rank_hi) s_con[rank - rank_lo] = meta;
-            }
-            ncon += (int)__popcll(bal);
-            hc = hn; rc = rn; kc = kn;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        return ncon;
-    };
-    // Address of a staged contributor's {L, L cos, L sin}: the candidate's
-    // snapshot (kind 0) or first in-chunk flow (kind 1), or an event's flow
-    // (kind 2); every form is three consecutive doubles.
-    auto value_ptr = [&](uint32_t en) -> const double * {
-        const uint32_t kind = (en >> 25) & 3u, ref = en & kRefMask;
-        const double *pc = reinterpret_cast<const double *>(cval + ref) + 3 * (kind & 1);
-        const double *pe = reinterpret_cast<const double *>(c.evf + ev0 + ref);
-        return kind == 2 ? pe : pc;
-    };
-    // ---- phase B: the per-scale sums in the reference's order.  vFlow.cpp:998-
-    // 1021 accumulates each scale from 0, cell by cell, i ascending then j
-    // ascending.  The staged list holds the contributors of the largest window in
-    // exactly that order (row slices in row order, ascending cells within a row;
-    // a cell the W-1 clip aliases into two rows appears twice, as the reference
-    // visits it twice), and scale k visits the subsequence of entries with
-    // k0 <= k.  Lane g*K + k (g = 0: L, 1: L cos(theta), 2: L sin(theta)) adds
-    // entry after entry and skips non-members: the reference's additions in the
-    // reference's order.  Values reach LDS 64 entries at a time; the loads of
-    // the next 64 are in flight while the current ones are summed.  Counts per
-    // scale are integers (ballots, any order).
     const int grp = lane / K < 2 ? lane / K : 2;  // lanes past 3K: a spare copy of group 2
     const int kk = lane - grp * K;
+    const uint64_t lt = (1ull << lane) - 1;
     double acc = 0.0;
     int cntk[K];  // wave-uniform
 #pragma unroll
     for (int k = 0; k < K; ++k) cntk[k] = 0;
-    int npass = 1, ncon_total = 0;
-    for (int pass = 0; pass < npass; ++pass) {
-        if (pass) {
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+    int ncon_total = 0;
+    // lanes without a contributor load the event's own flow (a valid address,
+    // finite values that a non-member fold adds as +0)
+    const double *const vdummy = reinterpret_cast<const double *>(c.evf + e);
+    // Flattened positions [f0, f0 + 64) per step: lane f's segment is the last
+    // non-empty one starting at or before f, i.e. the (number of segment
+    // starts <= f)-th one.
+    int mbase = 0;
+    auto locate = [&](int f0, int &row, int &k) {
+        const uint64_t mk = s_start[f0 >> 6];
+        const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
+        mbase += (int)__popcll(mk);
+        const uint32_t rs = s_row[m < 0 ? 0 : m];
+        row = (int)(rs >> 25);
+        k = f0 + lane + (int)(rs & 0x1FFFFFFu) - kRowBias;
+    };
+    int rc = 0, kc = 0;
+    CandHdr hc{};
+    if (total > 0) { locate(0, rc, kc); if (lane < total) hc = chdr[kc]; }
+    // the previous step's contributors: ballot, values, smallest scale
+    uint64_t pbal = 0;
+    double p0 = 0.0, p1 = 0.0, p2 = 0.0;
+    int pk0 = K;
+    for (int f0 = 0;; f0 += 64) {
+        const bool have = f0 < total;  // wave-uniform
+        bool con = false;
+        int k0 = K;
+        const double *vp = vdummy;
+        if (have && f0 + lane < total) {
+            uint32_t tq;
+            bool ok;
+            if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; vp = &cval[kc].L_snap; }
+            else if (!(hc.lin & kCandMore)) { ok = (hc.lin & kCandOneOk) != 0; tq = hc.t1; vp = &cval[kc].L1; }
+            else {  // several events at the cell inside the chunk: search its run
+                const CandVal &cv = cval[kc];
+                const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
+                const FlowCell fe = c.evf[sev];
+                ok = fe.L > 0; tq = fe.t; vp = &c.evf[sev].L;
+            }
+            if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
+            // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
+            const int64_t dt = (int64_t)teu - (int64_t)tq;
+            const int i = row_i0 + rc;
+            const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
+            if (ok && (uint64_t)(dt + 499) < 999u) {
+                const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
+                const int d = di > dj ? di : dj;
+                k0 = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);  // smallest scale containing the cell: ceil(d / J)
+                con = true;
+            }
         }
-        ncon_total = collect(pass);
-#if FARMS_POOL_STOP == 2
-        if (lane == 0) c.scale[e] = ncon_total;  // ablation: row setup + phase A
-        return;
-#endif
-        npass = ncon_total > kPoolCap ? (ncon_total + kPoolCap - 1) / kPoolCap : 1;
-        const int nb = (ncon_total < (pass + 1) * kPoolCap ? ncon_total : (pass + 1) * kPoolCap) - pass * kPoolCap;
-        // entry b0 + lane of the sub-batch at b0: its values and k0 (K: in no scale)
-        double w0 = 0.0, w1 = 0.0, w2 = 0.0;
-        int wk = K;
-        auto fetch = [&](int b0) {
-            const int b = b0 + lane;
-            const uint32_t en = b < nb ? s_con[b] : pack_con((uint32_t)(e - ev0), 2u, (uint32_t)K);
-            const double *pv = value_ptr(en);
-            w0 = pv[0]; w1 = pv[1]; w2 = pv[2];
-            wk = (int)(en >> 27);
-        };
-        if (nb > 0) fetch(0);
-        for (int b0 = 0; b0 < nb; b0 += 64) {
+        if (!con) vp = vdummy;
+        // this step's values and the next step's headers: both in flight during
+        // the fold below (unconditional loads: a load under a branch would be
+        // waited for at the branch end)
+        const double v0 = vp[0], v1 = vp[1], v2 = vp[2];
+        int rn = 0, kn = 0;
+        CandHdr hn{};
+        if (f0 + 64 < total) { locate(f0 + 64, rn, kn); if (f0 + 64 + lane < total) hn = chdr[kn]; }
+        // ---- stage and fold the previous step's contributors
+        if (pbal) {
+            const int cnt = (int)__popcll(pbal);
+            const bool pc = (pbal >> lane) & 1;
 #pragma unroll
-            for (int k = 0; k < K; ++k) cntk[k] += (int)__popcll(__ballot(wk <= k));
-            // the previous sub-batch's reads are done (wave-private LDS)
+            for (int k = 0; k < K; ++k) cntk[k] += (int)__popcll(__ballot(pc && pk0 <= k));
+            // every lane writes one slot: contributors [0, cnt) in rank order,
+            // the others after them with k0 = K (in no scale)
+            const int slot = pc ? (int)__popcll(pbal & lt) : cnt + (int)__popcll(~pbal & lt);
+            // the previous fold's LDS reads are done (wave-private LDS)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            s_val[3 * lane] = w0; s_val[3 * lane + 1] = w1; s_val[3 * lane + 2] = w2;
-            s_k0[lane] = (uint8_t)wk;
+            s_val[3 * slot] = p0; s_val[3 * slot + 1] = p1; s_val[3 * slot + 2] = p2;
+            s_k0[slot] = (uint8_t)(pc ? pk0 : K);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (b0 + 64 < nb) fetch(b0 + 64);
-            const int cnt = __builtin_amdgcn_readfirstlane(min(64, nb - b0));  // wave-uniform
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
             // Member entries are added as fma(v, 1, acc) = acc + v (one
             // rounding), non-members as fma(v, 0, acc) = acc + (+-0) = acc: acc
@@ -1912,19 +1842,25 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             // the reference's conditional one (valid flows are finite).  The
             // multiplier is off the dependency chain: one fma per entry on it.
 #pragma unroll 1
-            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // entries past cnt have k0 = K: no scale adds them
+            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // slots past cnt: k0 = K
                 uint32_t kw[FARMS_POOL_UNROLL / 4];
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL / 4; ++u) kw[u] = k4p[(r >> 2) + u];
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
-                    const int k0 = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
+                    const int k0u = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
                     const double v = s_val[3 * (r + u) + grp];
-                    const double m = kk >= k0 ? 1.0 : 0.0;
+                    const double m = kk >= k0u ? 1.0 : 0.0;
                     acc = __builtin_fma(v, m, acc);
                 }
             }
+            ncon_total += cnt;
         }
+        if (!have) break;
+        pbal = __ballot(con);
+        p0 = v0; p1 = v1; p2 = v2;
+        pk0 = k0;
+        hc = hn; rc = rn; kc = kn;
     }
     // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
     // the winner is the lowest k whose mean equals the maximum, if it is > 0
@@ -1960,14 +1896,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 // Per-event pooling: the row table of the event's own window, then the event.
 template <int K>
 __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
-                                           int ev0, uint64_t *s_start, uint32_t *s_row, uint32_t *s_con,
-                                           double *s_val, uint8_t *s_k0) {
+                                           int ev0, uint64_t *s_start, uint32_t *s_row, double *s_val,
+                                           uint8_t *s_k0) {
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nullptr);
-    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, 0, total, 0, j_lo, j_hi, ev0, s_start, s_row, s_con, s_val,
-                s_k0);
+    const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0);
 }
 
 // One wavefront per work-order position of [c0, c1) (events of a chunk in
@@ -1976,14 +1911,17 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #ifndef FARMS_POOL_WAVES
 #define FARMS_POOL_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
+#ifndef FARMS_POOL_VGPR_FLOOR
+#define FARMS_POOL_VGPR_FLOOR "v79"  // k_pool occupancy cap (see k_pool)
+#endif
 #ifndef FARMS_POOL_WPB
 #define FARMS_POOL_WPB 1  // waves (events) per k_pool workgroup: one, so that a finished event frees its slot at once
 #endif
 template <int K>
 __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
-    // LDS per wave, sized for maxWindow M at launch (pool_lds_bytes): segment-
-    // start bitmap over the flattened window, <= 2 row segments per window
-    // row, kPoolCap staged contributors, the values and k0 of 64 of them
+    // LDS per wave, sized for maxWindow M at launch: segment-start bitmap over
+    // the flattened window, <= 2 row segments per window row, the values and
+    // k0 of one step's 64 staged entries
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1999,91 +1937,18 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     asm volatile("" ::"v"(vld), "v"(ex), "v"(ey), "v"(teu));
     if (!vld) return;
     if (ex < c.own_lo || ex >= c.own_hi) return;
+    // Occupancy cap: the kernel allocates at least 80 VGPRs, i.e. at most 6
+    // pooling waves per SIMD (70 would allow 7).  The fit sweep's waves need
+    // the room: each of its 1,500 launches per C3 step waits for its slowest
+    // wave, so crowding them stretches the whole pipeline (measured at C3:
+    // 6 waves/SIMD 109.9 ms per step, 7: 122.0, 5: 113.9).
+    asm volatile("" ::: FARMS_POOL_VGPR_FLOOR);
     const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolCap / 2 + kPoolValWords);
+    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolValWords);
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
-    uint32_t *s_con = reinterpret_cast<uint32_t *>(s_start + nbw + nrs);
-    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + kPoolCap / 2);
+    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
-    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_con, s_val, s_k0);
-}
-
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-// Group pooling: one wavefront per pooling group, a run of work-order
-// positions with the same (pooling chunk, tile) key (split every
-// c.group_split positions).  The events of a group sit within one tile, so
-// their windows share almost every row: the wave builds the row table of the
-// union of its valid owned events' windows once (pool_rows), then pools each
-// of those events from it (pool_one restricted to the event's rows and
-// columns).  Same contributor lists in the same order as per-event pooling:
-// bitwise the same records.  Requires 2M + tile <= 128 union rows.
-template <int K>
-__global__ __launch_bounds__(256, FARMS_POOL_WAVES) void k_pool_grp(Ctx c, int g0, int g1) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
-    const int nbw = c.pool_bw, nrs = c.pool_rs, nri = c.pool_ri;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int g = g0 + work_block() * 4 + wv;
-    if (g >= g1) return;
-    const int ws = c.gstart[g], we = c.gstart[g + 1];
-    const int W = c.W, M = c.M;
-    // union of the windows of the group's valid owned events
-    int xmn = INT_MAX, xmx = INT_MIN, ymn = INT_MAX, ymx = INT_MIN;
-    bool any = false;
-    for (int w0 = ws; w0 < we; w0 += 64) {
-        const int w = w0 + lane;
-        uint32_t vld = 0;
-        int ex = 0, ey = 0;
-        if (w < we) {
-            const int e = c.Q[w];
-            vld = c.valid[e]; ex = c.x[e]; ey = c.y[e];
-        }
-        const bool ok = vld && ex >= c.own_lo && ex < c.own_hi;
-        if (ok) { xmn = min(xmn, ex); xmx = max(xmx, ex); ymn = min(ymn, ey); ymx = max(ymx, ey); }
-        any = any || __ballot(ok) != 0;
-    }
-    if (!any) return;
-    xmn = wave_min_i(xmn); xmx = wave_max_i(xmx); ymn = wave_min_i(ymn); ymx = wave_max_i(ymx);
-    const int i_lo = max(0, xmn - M), i_hi = min(W - 1, xmx + M);
-    const int j_lo = max(0, ymn - M), j_hi = min(W - 1, ymx + M);
-    const int buf = (ws / c.C2) % c.NB;
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + nri + kPoolCap / 2 + kPoolValWords);
-    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
-    int2 *s_rinfo = reinterpret_cast<int2 *>(s_start + nbw + nrs);
-    uint32_t *s_con = reinterpret_cast<uint32_t *>(s_start + nbw + nrs + nri);
-    double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs + nri + kPoolCap / 2);
-    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
-    pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, s_rinfo);
-    for (int w0 = ws; w0 < we; w0 += 64) {
-        const int w = w0 + lane;
-        uint32_t vld = 0, te = 0;
-        int e = 0, ex = 0, ey = 0;
-        if (w < we) {
-            e = c.Q[w];
-            vld = c.valid[e]; ex = c.x[e]; ey = c.y[e]; te = c.t[e];
-        }
-        uint64_t bal = __ballot(vld && ex >= c.own_lo && ex < c.own_hi);
-        while (bal) {
-            const int l = __builtin_ctzll(bal);
-            bal &= bal - 1;
-            const int el = __builtin_amdgcn_readlane(e, l), xl = __builtin_amdgcn_readlane(ex, l),
-                      yl = __builtin_amdgcn_readlane(ey, l);
-            const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane((int)te, l);
-            const int r0 = max(xl - M, i_lo) - i_lo, r1 = min(xl + M, i_hi) - i_lo;
-            const int2 a = s_rinfo[r0], b = s_rinfo[r1 + 1];
-            pool_one<K>(c, el, xl, yl, tl, buf, lane, i_lo, a.x, b.x, a.y, max(0, yl - M), min(W - 1, yl + M),
-                        (ws / c.C2) * c.C2, s_start, s_row, s_con, s_val, s_k0);
-        }
-    }
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -2261,13 +2126,6 @@ struct farms_handle {
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     int tile_bits = 0;
     int tile_shift = 3;       // work-order tile: 2^tile_shift square (FARMS_POOL_TILE)
-    bool pool_groups = false; // FARMS_POOL_GROUPS=1: k_pool_grp (measured 1.5x slower than per-event
-                              // k_pool at C3, DESIGN.md §8: fewer resident waves, events serial per wave)
-    int group_split = 64;    // work-order positions per pooling group at most (FARMS_GROUP_SPLIT)
-    uint8_t *gflags = nullptr;
-    int32_t *gstart = nullptr, *chunk_g0 = nullptr;
-    int *d_ng = nullptr;
-    std::vector<int32_t> chunk_g0_h;
     uint8_t *valid = nullptr;
     FlowCell *evf = nullptr;
     int2 *dbg_tc = nullptr;
@@ -2311,7 +2169,6 @@ void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->pos); dfree(h->prev); dfree(h->next);
     dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted); dfree(h->tprev);
-    dfree(h->gflags); dfree(h->gstart); dfree(h->chunk_g0); dfree(h->d_ng);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2338,9 +2195,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
         (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
-        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap))) ||
-        (rc = dalloc(&h->gflags, cap)) || (rc = dalloc(&h->gstart, cap + 1)) || (rc = dalloc(&h->chunk_g0, nch + 1)) ||
-        (rc = dalloc(&h->d_ng, 1))) {
+        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap)))) {
         free_workspace(h);
         return rc;
     }
@@ -2351,10 +2206,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
                                               end_bit_for(h->WH), h->stream));
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, h->wkey, h->wkey_sorted, h->iota, h->Q, (int)cap, 0,
                                               32, h->stream));
-    size_t bytes3 = 0;
-    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, bytes3, hipcub::CountingInputIterator<int32_t>(0), h->gflags,
-                                         h->gstart, h->d_ng, (int)cap, h->stream));
-    bytes = std::max(bytes, std::max(bytes2, bytes3));
+    bytes = std::max(bytes, bytes2);
     if ((rc = dalloc((uint8_t **)&h->cub_tmp, bytes))) { free_workspace(h); return rc; }
     h->cub_bytes = bytes;
     h->cap = cap;
@@ -2377,28 +2229,11 @@ int reset_surfaces(farms_handle *h) {
 template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
-    const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolCap / 2 + kPoolValWords);
+    const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
     hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, FARMS_POOL_WPB)), dim3(64 * FARMS_POOL_WPB), lds, s, c, c0, c1);
 }
 
-template <int K>
-void launch_pool_grp(const Ctx &c, int g0, int g1, hipStream_t s) {
-    const size_t lds = 4 * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + c.pool_ri + kPoolCap / 2 + kPoolValWords);
-    if (g1 > g0) hipLaunchKernelGGL(k_pool_grp<K>, dim3(ceil_div(g1 - g0, 4)), dim3(256), lds, s, c, g0, g1);
-}
-
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
-pool_launcher pool_grp_for(int K) {
-    switch (K) {
-    case 1: return launch_pool_grp<1>;   case 2: return launch_pool_grp<2>;   case 3: return launch_pool_grp<3>;
-    case 4: return launch_pool_grp<4>;   case 5: return launch_pool_grp<5>;   case 6: return launch_pool_grp<6>;
-    case 7: return launch_pool_grp<7>;   case 8: return launch_pool_grp<8>;   case 9: return launch_pool_grp<9>;
-    case 10: return launch_pool_grp<10>; case 11: return launch_pool_grp<11>; case 12: return launch_pool_grp<12>;
-    case 13: return launch_pool_grp<13>; case 14: return launch_pool_grp<14>; case 15: return launch_pool_grp<15>;
-    case 16: return launch_pool_grp<16>;
-    default: return nullptr;
-    }
-}
 pool_launcher pool_for(int K) {
     switch (K) {
     case 1: return launch_pool<1>;   case 2: return launch_pool<2>;   case 3: return launch_pool<3>;
@@ -2484,12 +2319,9 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
-    // a group's union window spans <= 2M + 2^tile_shift rows and columns
-    const int span = h->pool_groups ? 2 * h->M + (1 << h->tile_shift) : 2 * h->M + 1;
+    const int span = 2 * h->M + 1;  // pooling window rows and columns
     c.pool_bw = (span * span + 63) / 64;  // flattened window positions
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
-    c.pool_ri = h->pool_groups ? span + 1 : 0;
-    c.gstart = h->gstart;
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
@@ -2544,19 +2376,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
                                                   h->tile_bits + cb, s));
     }
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
-    if (h->pool_groups) {  // pooling groups and each pooling chunk's first group (read back: launch bounds)
-        hipLaunchKernelGGL(k_group_flags, dim3(ceil_div(n, 256)), dim3(256), 0, s, h->wkey_sorted, n, h->group_split,
-                           h->gflags);
-        size_t b3 = h->cub_bytes;
-        HIPCHK(hipcub::DeviceSelect::Flagged(h->cub_tmp, b3, hipcub::CountingInputIterator<int32_t>(0), h->gflags,
-                                             h->gstart, h->d_ng, n, s));
-        hipLaunchKernelGGL(k_group_index, dim3(ceil_div(n, 256)), dim3(256), 0, s, n, h->d_ng, h->gstart, h->pool_chunk,
-                           h->chunk_g0, n_pool_chunks);
-        h->chunk_g0_h.resize((size_t)n_pool_chunks + 1);
-        HIPCHK(hipMemcpyAsync(h->chunk_g0_h.data(), h->chunk_g0, sizeof(int32_t) * (n_pool_chunks + 1),
-                              hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-    }
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
     }  // prep
@@ -2575,7 +2394,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const char *ser = getenv("FARMS_SERIALIZE");
     const bool serial = ser && ser[0] == '1';
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
-    pool_launcher pl = h->pool_groups ? pool_grp_for(h->K) : pool_for(h->K);
+    pool_launcher pl = pool_for(h->K);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
     const bool fit_quad = !(fq && fq[0] == '0');
@@ -2639,8 +2458,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
-        if (h->pool_groups) pl(c, h->chunk_g0_h[ch0], h->chunk_g0_h[ch1], sp);
-        else pl(c, p0, p1, sp);
+        pl(c, p0, p1, sp);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
         hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
@@ -2782,9 +2600,6 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     if (const char *v = getenv("FARMS_POOL_TILE")) h->tile_shift = std::max(1, std::min(atoi(v), 6));
-    if (const char *v = getenv("FARMS_GROUP_SPLIT")) h->group_split = std::max(1, atoi(v));
-    if (const char *v = getenv("FARMS_POOL_GROUPS")) h->pool_groups = v[0] != '0';
-    if (2 * h->M + (1 << h->tile_shift) > 128) h->pool_groups = false;  // union rows: 2 per lane
     {
         const int tm = (1 << h->tile_shift) - 1;
         const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);

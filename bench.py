@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--fit-chunk", type=int, default=0)
     ap.add_argument("--pool-chunk", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
+    ap.add_argument("--parity-sample", type=int, default=300_000,
+                    help="N > 1: rank 0 checks its records of the stream's first K events against the oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", choices=("segments", "strips", "strips-recompute"), default="segments",
                     help="N > 1: temporal segments (time-ordered streams), x-strips with an RCCL exchange of "
@@ -180,6 +182,35 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
     return r
 
 
+def parity_multi(args, cfg: int, sh: dict, out, owned_mask) -> dict:
+    """N > 1, rank 0: its owned records among the stream's first K events
+    against the oracle run on that prefix (the path is causal: a prefix of the
+    whole run equals a run of the prefix).  Exercises the exchange: rank 0's
+    records read halo flows (strips) or are checked across its segment's end."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import OracleFlow
+    from parity import compare
+
+    W, H = SENSOR[cfg]
+    jump, maxw = (25, 50) if cfg == 5 else (5, 50)
+    sp = farms.synth_params(cfg)
+    sp.n_events = sh["n_stream"]
+    k = min(args.parity_sample, sh["n_stream"])
+    ev, _, t_first = farms.synth_select(sp, 0, k)
+    x, y, t, p = ev.relative(t_first)
+    ref = OracleFlow(H, W, FILTER[cfg], 5, jump, maxw).process(x, y, t, p)
+    sel = np.flatnonzero(owned_mask & (sh["gidx"] < k))
+    g = sh["gidx"][sel]
+    gpu = {"x": x[g], "y": y[g], "t": t[g], "p": p[g]}
+    gpu.update({c: out[c].cpu().numpy()[sel] for c in farms.COLUMNS[4:]})
+    rep = compare(gpu, {c: np.asarray(ref[c])[g] for c in farms.COLUMNS})
+    return {"events_compared": int(sel.size), "stream_prefix": k, "valid_events": rep["valid_ref"],
+            "valid_mismatch": rep["valid_mismatch"], "max_dtheta_true_rad": rep["theta_true_max_abs"],
+            "max_rel_r_true": rep["r_true_max_rel"], "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"],
+            "what": "rank 0's owned records of the stream's first K events vs the oracle on that prefix"}
+
+
 def host_path(fm, x, y, t, p, steps: int) -> dict:
     """The boundary as the CLI uses it (vFlow.cpp:214-416): host arrays in,
     host records out through farms_process — pinned staging, H2D, the kernels,
@@ -213,7 +244,8 @@ def rank_share(args, cfg: int, world: int, rank: int) -> dict:
     per_gpu = args.events or (int(sp.n_events) if cfg in (1, 2, 3) else 50_000_000)
     n = per_gpu * world
     sp.n_events = n
-    sh = {"per_gpu": per_gpu, "n_stream": n, "region": None, "owned": None, "seg": None, "cpu_sample": None}
+    sh = {"per_gpu": per_gpu, "n_stream": n, "region": None, "owned": None, "seg": None, "cpu_sample": None,
+          "gidx": None}
     if world == 1:
         ev = farms.synth_generate(sp)
         sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative()
@@ -227,6 +259,7 @@ def rank_share(args, cfg: int, world: int, rank: int) -> dict:
         seg, n_head = segments.plan_rank(t, lo, n, world, rank)  # raises on an unordered stream
         sl = slice(seg.warm - lo, seg.end - lo)
         sh["x"], sh["y"], sh["t"], sh["p"] = x[sl], y[sl], t[sl], p[sl]
+        sh["gidx"] = np.arange(seg.warm, seg.end, dtype=np.int64)
         sh.update(split="segments", seg=seg, n_head=n_head, n_owned=seg.end - seg.start,
                   label=(f"{world} temporal segments of the time-ordered stream: per step the ranks' last-stamp "
                          f"surfaces are all-gathered and each rank starts from the merged SAE plus a re-fitted "
@@ -235,8 +268,9 @@ def rank_share(args, cfg: int, world: int, rank: int) -> dict:
         exch = args.split == "strips"
         plan = strips.plan_hist(farms.synth_column_hist(sp), H, world, fs, maxw, exchange=exch)
         strip = plan[rank]
-        ev, _, t_first = farms.synth_select(sp, 0, n, strip.reg_lo, strip.reg_hi)
+        ev, gidx, t_first = farms.synth_select(sp, 0, n, strip.reg_lo, strip.reg_hi)
         sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative(t_first)
+        sh["gidx"] = gidx
         hl, hr = strips.halo(fs, maxw, W, H, exchange=exch)
         sh.update(split=args.split, region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi),
                   n_owned=int(strips.owned_mask(sh["x"], strip).sum()))
@@ -420,6 +454,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ref, line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
         line["parity"] = parity_vs_cpu(ref, out, len(cpu_sample))
+    if world > 1 and rank == 0 and args.parity_sample > 0:
+        if seg is not None:
+            mask = np.zeros(n, bool)
+            mask[seg.n_warm:] = True
+        else:
+            mask = (x >= sh["owned"][0]) & (x < sh["owned"][1])
+        line["parity"] = parity_multi(args, cfg, sh, out, mask)
     if world > 1:
         line["detail"]["rank0_stored_events"] = n
         line["detail"]["rank0_owned_events"] = n_owned

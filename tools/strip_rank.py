@@ -33,6 +33,8 @@ ap.add_argument("--n", type=int, default=8, help="strips (simulated GPUs)")
 ap.add_argument("--ranks", default="", help="comma list; default: all")
 ap.add_argument("--events", type=int, default=50_000_000, help="events per GPU")
 ap.add_argument("--fit", default="0")
+ap.add_argument("--pool", type=int, default=0, help="pooling chunk (0: the engine's default)")
+ap.add_argument("--batch", type=int, default=0, help="pooling chunks per super-chunk (0: default)")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--split", choices=("strips", "strips-recompute", "segments"), default="strips")
 a = ap.parse_args()
@@ -73,8 +75,8 @@ for fc in [int(v) for v in a.fit.split(",")]:
         n = len(dx)
         out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
                for c in farms.COLUMNS[4:]}
-        fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, fit_chunk=fc,
-                               region=region, owned=own, import_halo=exch)
+        fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, fit_chunk=fc, pool_chunk=a.pool,
+                               pool_batch=a.batch, region=region, owned=own, import_halo=exch)
         if exch:  # realistic halo flows: a handle that fits the halo itself
             halo = np.flatnonzero(~strips.owned_mask(x, s)).astype(np.int32)
             hidx = torch.from_numpy(halo).to(dev)
@@ -117,7 +119,7 @@ for fc in [int(v) for v in a.fit.split(",")]:
         st = fm.stats()
         fm.close()
         worst = max(worst, best)
-        print(json.dumps({"n": a.n, "rank": r, "fit_chunk": fc, "split": a.split, "range": cols, "stored": n,
+        print(json.dumps({"n": a.n, "rank": r, "fit_chunk": fc, "pool_chunk": a.pool, "batch": a.batch, "split": a.split, "range": cols, "stored": n,
                           "owned": owned, "ms": round(best * 1e3, 1), "ms_fit_sweep": round(st["ms_fit"], 1),
                           "ms_pool_sweep": round(st["ms_pool"], 1), "ms_fit_k": round(st["ms_fit_kernel"], 1),
                           "ms_pool_k": round(st["ms_pool_kernel"], 1)}), flush=True)

@@ -171,10 +171,13 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
         waves = max(sq["SQ_WAVES"], 1.0)
         wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
         # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; a wave64
-        # VALU instruction issues over 4 of them
+        # VALU instruction occupies a SIMD-32 for 2 of them (fp64 FMA: 4), so
+        # this utilisation is a lower bound of the VALU pipe's busy fraction
         simd_cycles = 1024 * 2.4e9 * avg_us * 1e-6
         r["issue"] = {"valu_insts_per_wave": round(sq["SQ_INSTS_VALU"] / waves, 1),
-                      "valu_issue_util": round(4.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
+                      "valu_issue_util": round(2.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
+                      "binds": "latency: waves wait on dependent L2 loads and on the fp64 fold chain "
+                               "(wait_any + wait_inst > active); not HBM, not VALU throughput",
                       "wait_any_frac": round(sq["SQ_WAIT_ANY"] / wave_cyc, 4),
                       "wait_inst_frac": round(sq["SQ_WAIT_INST_ANY"] / wave_cyc, 4),
                       "active_inst_frac": round(sq["SQ_ACTIVE_INST_ANY"] / wave_cyc, 4),

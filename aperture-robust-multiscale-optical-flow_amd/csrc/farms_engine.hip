@@ -165,9 +165,13 @@ struct Ctx {
     const uint32_t *pix;   // x*H + y per event
     const uint32_t *skey;  // pixel ids, sorted
     const int32_t *P;      // event ids sorted by (pixel, id)
-    const int32_t *pos;    // inverse of P
     const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
-    const int32_t *prev, *next;
+    // per event, one 16-B record (k_link): {position in P, previous and next
+    // event at the pixel (-1 / INT_MAX: none), tpv}; tpv = the stamp the
+    // pixel's SAE holds just before the event (the previous event's, or, for
+    // the pixel's first event of the call, the snapshot's in serial mode, 0 in
+    // batch mode, where it is not read)
+    const int4 *link;
     SaeCell *cells;        // SAE snapshot + in-chunk first event, per cell
     const int2 *PT;        // per position in P: {event id, t}
     FlowCell *fsnap;       // flow snapshot
@@ -185,11 +189,10 @@ struct Ctx {
     int NB, C2;            // ring size, events per pooling chunk
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
-    // serial mode (vFlowManager::run, vFlow.cpp:465-826): per event, the stamp
-    // its pixel's lastEventTime holds while the event is pooled (written only
-    // after pooling, :790): the previous event's there, else the stamp before
-    // the call.  nullptr in batch mode.
-    const uint32_t *tprev;
+    // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
+    // with its pixel's lastEventTime still holding link.w, the stamp before it
+    // (written only after pooling, :790)
+    bool serial;
     // outputs
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
     int32_t *scale;
@@ -287,21 +290,26 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
     iota[e] = e;
 }
 
-__global__ void k_link(Ctx c, int32_t *pos, int32_t *prev, int32_t *next, int2 *PT, uint32_t *tprev) {
+// Per position k of P (events sorted by pixel, then index): PT[k] = {event,
+// stamp}, and the event's link record, one 16-B scatter per event.  The stamp
+// of the previous position comes from the neighbouring lane.
+__global__ void k_link(Ctx c, int4 *link, int2 *PT, bool serial) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= c.n) return;
-    const int e = c.P[k];
+    const bool in = k < c.n;
+    const int e = in ? c.P[k] : 0;
+    const uint32_t te = in ? c.t[e] : 0u;
+    uint32_t tp = (uint32_t)__shfl_up((int)te, 1, 64);
+    if ((threadIdx.x & 63) == 0 && in && k > 0) tp = c.t[c.P[k - 1]];
+    if (!in) return;
     const uint32_t q = c.skey[k];
-    pos[e] = k;
-    PT[k] = make_int2(e, (int)c.t[e]);
+    PT[k] = make_int2(e, (int)te);
     const bool first = !(k > 0 && c.skey[k - 1] == q), last = !(k + 1 < c.n && c.skey[k + 1] == q);
-    prev[e] = first ? -1 : c.P[k - 1];
     // serial mode: lastEventTime[x][y] while e is pooled.  Before the call it
     // is the flow snapshot's stamp (the last event at q, 0 if none, or the
     // first line's stamp set by farms_serial_first); the pooling chain only
     // advances fsnap after prep.
-    if (tprev) tprev[e] = first ? c.fsnap[q].t : c.t[c.P[k - 1]];
-    next[e] = last ? INT_MAX : c.P[k + 1];
+    const uint32_t tpv = first ? (serial ? c.fsnap[q].t : 0u) : tp;
+    link[e] = make_int4(k, first ? -1 : c.P[k - 1], last ? INT_MAX : c.P[k + 1], (int)tpv);
     if (first) c.pcur[q] = k;  // the pooling chain's run bounds of the cell
     if (last) c.pend[q] = k;
 }
@@ -334,12 +342,14 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
     }
 }
 
-// Fit sweep, between chunks (one launch): for chunk f = [c0, c1), record at
+// Fit sweep, before chunk f (double-buffered SAE: chunk f reads buffer f % 2):
+// for chunk f = [c0, c1), record at
 // every touched pixel its first two in-chunk events inline and the bounds of
 // its in-chunk run in P, and set the SAE snapshot to the pixel's last event
-// before the chunk (prev of its first event); for chunk f-1 = [p0, c0), set
-// the snapshot of pixels it touched that chunk f does not touch.  The two
-// parts write disjoint cells.
+// before the chunk (prev of its first event); for the events [p0, c0) before
+// it (chunks f-2 and f-1: the buffer last served chunk f-2), set the snapshot
+// of the pixels they touched that chunk f does not touch to their last event.
+// The two parts write disjoint cells.
 // Wave priority of the fit sweep's kernels: each fit launch waits for its
 // predecessor's slowest wave, and those waves share their SIMDs with the
 // pooling waves of the stream beside it; raising their issue priority keeps
@@ -354,14 +364,13 @@ __device__ __forceinline__ void fit_prio() {
 #define FARMS_CHAIN_PRIO 0
 #endif
 
-__global__ void k_fit_prep(Ctx c, int p0, int c0, int c1, uint32_t seq) {
-    fit_prio();
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq,
+                                                int i) {
     const int ep = p0 + i;
     if (ep < c0) {
-        const int nx = c.next[ep];
+        const int nx = c.link[ep].z;
         if (nx >= c0 && nx >= c1) {  // last event of chunk f-1 at a pixel chunk f does not touch
-            SaeCell *cell = &c.cells[c.pix[ep]];
+            SaeCell *cell = &cells[c.pix[ep]];
             cell->tag |= 0x80000000u;
             cell->tsnap = c.t[ep];
         }
@@ -369,27 +378,45 @@ __global__ void k_fit_prep(Ctx c, int p0, int c0, int c1, uint32_t seq) {
     const int e = c0 + i;
     if (e >= c1) return;
     const uint32_t q = c.pix[e];
-    const int nx = c.next[e];
-    if (c.prev[e] < c0) {  // first event of the pixel in the chunk
-        SaeCell *cell = &c.cells[q];
-        const int pv = c.prev[e];
-        if (pv >= 0) {
+    const int4 lk = c.link[e];  // {pos, prev, next, stamp before}
+    const int nx = lk.z;
+    if (lk.y < c0) {  // first event of the pixel in the chunk
+        SaeCell *cell = &cells[q];
+        if (lk.y >= 0) {
             cell->tag = seq | 0x80000000u;
-            cell->tsnap = c.t[pv];
+            cell->tsnap = (uint32_t)lk.w;
         } else {  // no earlier event in this call: keep the snapshot of earlier calls
             cell->tag = (cell->tag & 0x80000000u) | seq;
         }
         cell->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
         cell->t1 = c.t[e];
-        cell->run_lo = c.pos[e];
+        cell->run_lo = lk.x;
         if (nx < c1) {  // and the second one
-            const int nn = c.next[nx];
+            const int nn = c.link[nx].z;
             cell->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
             cell->t2 = c.t[nx];
         }
     }
-    if (nx >= c1) c.cells[q].run_hi = c.pos[e];
+    if (nx >= c1) cells[q].run_hi = lk.x;
 }
+
+// The prep of one fit chunk as its own launch (the first chunk of a call, the
+// final commits, the fit paths without a merged prep).
+__global__ void k_fit_prep(Ctx c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq) {
+    fit_prio();
+    fit_prep_thread(c, cells, p0, c0, c1, seq, (int)(blockIdx.x * blockDim.x + threadIdx.x));
+}
+
+// The prep of fit chunk f+1 riding on the launch of fit chunk f (blocks past
+// the fit's grid): it writes the other SAE buffer, which the fit of chunk f
+// does not read, and the fit of chunk f-1 (the buffer's last reader) finished
+// with the previous launch.
+struct FitPrep {
+    SaeCell *cells;
+    int p0, c0, c1;
+    uint32_t seq;
+    int blocks;  // prep blocks after the fit's
+};
 
 // ---------------------------------------------------------------------------
 // Eigen 3.4 PartialPivLU<MatrixXd>::determinant() of the 3x3 normal matrix
@@ -1178,8 +1205,14 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
 #define FARMS_FIT_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
 template <int FR, bool UT>
-__global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq) {
+__global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
     fit_prio();
+    const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
+    if ((int)blockIdx.x >= G) {
+        fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
+                        ((int)blockIdx.x - G) * (int)blockDim.x + (int)threadIdx.x);
+        return;
+    }
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
@@ -1187,7 +1220,7 @@ __global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_qua
 #ifndef FARMS_FIT_XCD
 #define FARMS_FIT_XCD 1
 #endif
-    const int fb = FARMS_FIT_XCD ? xcd_block_grouped((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int fb = FARMS_FIT_XCD ? xcd_block_grouped((int)blockIdx.x, G) : (int)blockIdx.x;
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -1745,8 +1778,8 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     const int OFF = c.X0 * c.H;
     // serial mode: the own cell is pooled with the stamp its lastEventTime still
     // holds (the previous event's), not the event's own (vFlow.cpp:790 vs :264)
-    const uint32_t own_lin = c.tprev ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
-    const uint32_t own_tprev = c.tprev ? c.tprev[e] : 0u;
+    const uint32_t own_lin = c.serial ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
+    const uint32_t own_tprev = c.serial ? (uint32_t)c.link[e].w : 0u;
     (void)ev0;
 #if FARMS_POOL_STOP == 1
     if (lane == 0) c.scale[e] = total;  // ablation: row setup only
@@ -2029,7 +2062,8 @@ __global__ void k_seed_sae(Ctx c, const int64_t *stamp) {
     SaeCell cell{};
     cell.tag = s >= 0 ? 0x80000000u : 0u;  // chunk seq 0: never matches a chunk
     cell.tsnap = s >= 0 ? (uint32_t)s : 0u;
-    c.cells[q] = cell;
+    c.cells[q] = cell;  // both SAE buffers
+    c.cells[q + c.WH] = cell;
 }
 
 // lastEventTime surface for farms_get_last_event_time: stamp of the latest
@@ -2113,9 +2147,9 @@ struct farms_handle {
     int64_t cap = 0;
     int32_t *x = nullptr, *y = nullptr, *p = nullptr;
     uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
-    int32_t *iota = nullptr, *P = nullptr, *pos = nullptr, *prev = nullptr, *next = nullptr;
+    int32_t *iota = nullptr, *P = nullptr;
+    int4 *link = nullptr;
     int32_t *Q = nullptr;
-    uint32_t *tprev = nullptr;  // serial mode only
     // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
     const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
     const uint32_t *ph_t = nullptr;
@@ -2167,8 +2201,8 @@ void dfree(T *&p) {
 
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
-    dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->pos); dfree(h->prev); dfree(h->next);
-    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted); dfree(h->tprev);
+    dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->link);
+    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2190,12 +2224,12 @@ int ensure_capacity(farms_handle *h, int64_t n) {
     int rc;
     if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
         (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
-        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->pos, cap)) ||
+        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->link, cap)) ||
         (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
-        (rc = dalloc(&h->prev, cap)) || (rc = dalloc(&h->next, cap)) || (rc = dalloc(&h->valid, cap)) ||
+        (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
-        (rc = dalloc(&h->ctmax, nch)) || (h->prm.serial && (rc = dalloc(&h->tprev, cap)))) {
+        (rc = dalloc(&h->ctmax, nch))) {
         free_workspace(h);
         return rc;
     }
@@ -2215,7 +2249,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
 
 int reset_surfaces(farms_handle *h) {
     // tag 0: never visited, never touched (chunk seqs start at 1)
-    HIPCHK(hipMemsetAsync(h->cells, 0, sizeof(SaeCell) * h->WH, h->stream));
+    HIPCHK(hipMemsetAsync(h->cells, 0, 2 * sizeof(SaeCell) * h->WH, h->stream));  // both SAE buffers
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->pcur, 0, sizeof(int32_t) * h->WH, h->stream));
@@ -2246,20 +2280,23 @@ pool_launcher pool_for(int K) {
     }
 }
 
-void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile) {
+// Fit of chunk [c0, c1); pr.blocks > 0: with the next chunk's prep riding on
+// the same launch (quad path only; returns false when it did not take it).
+bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile,
+                FitPrep pr) {
     if (quad) {
-        const dim3 g(ceil_div(c1 - c0, kFitQS)), b(64 * FARMS_FIT_WPB);
+        const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks), b(64 * FARMS_FIT_WPB);
         switch (fr) {
-        case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq); return;
+        case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq, pr); return true;
         case 2:
-            if (union_tile) hipLaunchKernelGGL((k_fit_quad<2, true>), g, b, 0, s, c, c0, c1, seq);
-            else hipLaunchKernelGGL((k_fit_quad<2, false>), g, b, 0, s, c, c0, c1, seq);
-            return;
+            if (union_tile) hipLaunchKernelGGL((k_fit_quad<2, true>), g, b, 0, s, c, c0, c1, seq, pr);
+            else hipLaunchKernelGGL((k_fit_quad<2, false>), g, b, 0, s, c, c0, c1, seq, pr);
+            return true;
         case 3:
-            if (union_tile) hipLaunchKernelGGL((k_fit_quad<3, true>), g, b, 0, s, c, c0, c1, seq);
-            else hipLaunchKernelGGL((k_fit_quad<3, false>), g, b, 0, s, c, c0, c1, seq);
-            return;
-        default: return;
+            if (union_tile) hipLaunchKernelGGL((k_fit_quad<3, true>), g, b, 0, s, c, c0, c1, seq, pr);
+            else hipLaunchKernelGGL((k_fit_quad<3, false>), g, b, 0, s, c, c0, c1, seq, pr);
+            return true;
+        default: return false;
         }
     }
     const dim3 g(ceil_div(c1 - c0, 256)), b(256);
@@ -2269,6 +2306,7 @@ void launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t 
     case 3: hipLaunchKernelGGL(k_fit<3>, g, b, 0, s, c, c0, c1, seq); break;
     default: break;  // k_fit_wave
     }
+    return false;
 }
 
 int ensure_kernel_events(farms_handle *h, size_t count) {
@@ -2310,12 +2348,12 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
-    c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.pos = h->pos; c.prev = h->prev; c.next = h->next;
+    c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.link = h->link;
     c.Q = h->Q;
     c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.pcur = h->pcur; c.pend = h->pend;
-    c.tprev = h->prm.serial ? h->tprev : nullptr;
+    c.serial = h->prm.serial != 0;
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
@@ -2365,8 +2403,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
                                               end_bit_for(h->WH), s));
     HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
-    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pos, h->prev, h->next, h->PT,
-                       h->prm.serial ? h->tprev : nullptr);
+    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->link, h->PT, h->prm.serial != 0);
     {
         int cb = 1;
         while ((1 << cb) < n_pool_chunks) ++cb;
@@ -2402,22 +2439,48 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const bool fit_ut = !(fu && fu[0] == '0');
     int fit_launches = 0;
     auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
+    // The SAE is double-buffered by chunk parity (buffer f % 2 serves chunk f),
+    // so the prep of chunk f+1 rides on the launch of fit f: one launch per fit
+    // chunk.  Chunk seqs are base + f + 1.
+    const uint32_t seq_base = h->seq;
+    h->seq += (uint32_t)n_fit_chunks;
+    auto cells_of = [&](int f) { return h->cells + (size_t)(f & 1) * (size_t)h->WH; };
+    auto fit_start = [&](int f) { return f * h->fit_chunk; };
+    auto prep_of = [&](int f) {  // the prep of chunk f (into buffer f % 2); blocks for 64-thread blocks
+        FitPrep pr{cells_of(f), fit_start(std::max(f - 2, 0)), fit_start(f), fit_chunk_end(f), seq_base + f + 1, 0};
+        pr.blocks = ceil_div(std::max(pr.c1 - pr.c0, pr.c0 - pr.p0), 64);
+        return pr;
+    };
+    auto launch_prep = [&](const FitPrep &pr) {
+        hipLaunchKernelGGL(k_fit_prep, dim3(pr.blocks), dim3(64), 0, s, c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq);
+    };
     auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F
-        const int c0 = f * h->fit_chunk, c1 = fit_chunk_end(f), p0 = f > 0 ? (f - 1) * h->fit_chunk : 0;
-        const uint32_t seq = ++h->seq;
-        hipLaunchKernelGGL(k_fit_prep, dim3(ceil_div(std::max(c1 - c0, c0 - p0), 256)), dim3(256), 0, s, c, p0, c0,
-                           c1, seq);
+        const int c0 = fit_start(f), c1 = fit_chunk_end(f);
+        if (f == 0) launch_prep(prep_of(0));
+        Ctx cf = c;
+        cf.cells = cells_of(f);
+        FitPrep next{};
+        if (f + 1 < n_fit_chunks) next = prep_of(f + 1);
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f], s));
+        bool merged = false;
         if (fast_fit) {
-            launch_fit(c, h->fr, c0, c1, seq, s, fit_quad, fit_ut);
+            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
-            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, c, seq, h->Q + c0, c1 - c0);
+            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, h->Q + c0,
+                               c1 - c0);
         }
+        if (!merged && next.blocks > 0) launch_prep(next);
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
         HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
-        if (f == n_fit_chunks - 1) {  // SAE snapshot of the last chunk (streaming state)
-            hipLaunchKernelGGL(k_fit_prep, dim3(ceil_div(n - c0, 256)), dim3(256), 0, s, c, c0, n, n, 0u);
+        if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
+            FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
+            fin.blocks = ceil_div(n - c0, 64);
+            launch_prep(fin);
+            fin.cells = cells_of(f + 1);
+            fin.p0 = fit_start(std::max(f - 1, 0));
+            fin.blocks = ceil_div(n - fin.p0, 64);
+            launch_prep(fin);
             if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
         }
         return FARMS_OK;
@@ -2621,7 +2684,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
-    if ((rc = dalloc(&h->cells, h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
+    if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->pcur, h->WH)) || (rc = dalloc(&h->pend, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
         (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))

@@ -1646,8 +1646,58 @@ __device__ __forceinline__ double wave_max(double v) {
 #define FARMS_POOL_STOP 0  // ablation aid (variants only): 1 row setup only, 3 all but the folds
 #endif
 #ifndef FARMS_POOL_UNROLL
-#define FARMS_POOL_UNROLL 8  // phase B entries per loop trip (4 or 8; 64 must be a multiple)
+#define FARMS_POOL_UNROLL 8  // fold entries per loop trip (4 or 8; 64 must be a multiple)
 #endif
+#ifndef FARMS_POOL_FOLD_ASM
+#define FARMS_POOL_FOLD_ASM 1  // 0: the fold as masked fmas in C (A/B aid)
+#endif
+#if FARMS_POOL_FOLD_ASM && FARMS_POOL_UNROLL != 8
+#error "the asm fold takes 8 entries per trip"
+#endif
+// Fold of 8 staged entries into this lane's sum: entry u (smallest scale k0 =
+// byte u of kw0:kw1) is added iff kk >= k0, as an exec-masked v_add_f64: the
+// member test runs once per entry for all lanes (v_cmp into an SGPR mask, all
+// 8 before any exec change), then each add executes on the member lanes only,
+// bitwise the conditional add of the reference (vFlow.cpp:1005-1008) and one
+// fp64 add per entry on the dependency chain (the masked-fma form costs a
+// compare, a select and an fma).  exec is restored before the asm ends.  The
+// masks are subsets of exec (v_cmp writes 0 for inactive lanes), so exec is set
+// with s_mov_b64, which leaves SCC alone: the surrounding code may hold a
+// loop condition there (s_and_b64 would clobber it).
+__device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_t kw1, const double (&v)[8]) {
+    uint64_t m0, m1, m2, m3, m4, m5, m6, m7, sv;
+    asm volatile(
+        "v_cmp_ge_i32_sdwa %[m0], %[kk], %[kw0] src0_sel:DWORD src1_sel:BYTE_0\n"
+        "v_cmp_ge_i32_sdwa %[m1], %[kk], %[kw0] src0_sel:DWORD src1_sel:BYTE_1\n"
+        "v_cmp_ge_i32_sdwa %[m2], %[kk], %[kw0] src0_sel:DWORD src1_sel:BYTE_2\n"
+        "v_cmp_ge_i32_sdwa %[m3], %[kk], %[kw0] src0_sel:DWORD src1_sel:BYTE_3\n"
+        "v_cmp_ge_i32_sdwa %[m4], %[kk], %[kw1] src0_sel:DWORD src1_sel:BYTE_0\n"
+        "v_cmp_ge_i32_sdwa %[m5], %[kk], %[kw1] src0_sel:DWORD src1_sel:BYTE_1\n"
+        "v_cmp_ge_i32_sdwa %[m6], %[kk], %[kw1] src0_sel:DWORD src1_sel:BYTE_2\n"
+        "v_cmp_ge_i32_sdwa %[m7], %[kk], %[kw1] src0_sel:DWORD src1_sel:BYTE_3\n"
+        "s_mov_b64 %[sv], exec\n"
+        "s_mov_b64 exec, %[m0]\n"
+        "v_add_f64 %[acc], %[acc], %[v0]\n"
+        "s_mov_b64 exec, %[m1]\n"
+        "v_add_f64 %[acc], %[acc], %[v1]\n"
+        "s_mov_b64 exec, %[m2]\n"
+        "v_add_f64 %[acc], %[acc], %[v2]\n"
+        "s_mov_b64 exec, %[m3]\n"
+        "v_add_f64 %[acc], %[acc], %[v3]\n"
+        "s_mov_b64 exec, %[m4]\n"
+        "v_add_f64 %[acc], %[acc], %[v4]\n"
+        "s_mov_b64 exec, %[m5]\n"
+        "v_add_f64 %[acc], %[acc], %[v5]\n"
+        "s_mov_b64 exec, %[m6]\n"
+        "v_add_f64 %[acc], %[acc], %[v6]\n"
+        "s_mov_b64 exec, %[m7]\n"
+        "v_add_f64 %[acc], %[acc], %[v7]\n"
+        "s_mov_b64 exec, %[sv]\n"
+        : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [m4] "=&s"(m4),
+          [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [sv] "=&s"(sv)
+        : [kk] "v"(kk), [kw0] "v"(kw0), [kw1] "v"(kw1), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]),
+          [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7]));
+}
 // Row setup of a pooling window: the flattened candidate slices of rows
 // [i_lo, i_lo + nrows) (nrows <= 128), cells j in [j_lo, j_hi] of each row
 // (x-major; j already clipped to W-1 as vFlow.cpp:1000/1113 do, so for W > H a
@@ -1879,6 +1929,12 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 uint32_t kw[FARMS_POOL_UNROLL / 4];
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL / 4; ++u) kw[u] = k4p[(r >> 2) + u];
+#if FARMS_POOL_FOLD_ASM
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = s_val[3 * (r + u) + grp];
+                fold8(acc, kk, kw[0], kw[1], v);
+#else
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
                     const int k0u = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
@@ -1886,6 +1942,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                     const double m = kk >= k0u ? 1.0 : 0.0;
                     acc = __builtin_fma(v, m, acc);
                 }
+#endif
             }
             ncon_total += cnt;
         }

@@ -147,7 +147,7 @@ constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 // valid while candidate slots stay below 2^24 (W * H <= kMaxSlots)
 constexpr int kRowBias = 1 << 14;  // flattened positions of a window < 128 x 128
 constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
-constexpr int kPoolValWords = 3 * 64 + 8;  // k_pool staging: {L, L cos, L sin} and k0 of 64 entries, 8-B words
+constexpr int kPoolValWords = 4 * 64 + 8;  // k_pool staging: {L, L cos, L sin, 1} and k0 of 64 entries, 8-B words
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -1813,15 +1813,15 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
 //   in that order (row slices in row order, ascending cells within a row; a
 //   cell the W-1 clip aliases into two rows appears twice, as the reference
 //   visits it twice).  So every per-scale sum, mean and the first strict
-//   maximum are bitwise the reference's given the same local flows.  Counts
-//   per scale are integers (ballots, any order).
-// LDS (private to the wave): s_val / s_k0 the values and k0 of one step's
+//   maximum are bitwise the reference's given the same local flows.  Lanes
+//   3K + kk fold 1.0 per member: the contributor count of scale kk, exact.
+// LDS (private to the wave): s_val / s_k0 the values {L, L cos, L sin, 1} and k0 of one step's
 // 64 staged entries (contributors first, in rank order).
 template <int K>
 __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
                                          int row_i0, int total, int ev0, const uint64_t *s_start,
                                          const uint32_t *s_row, double *s_val, uint8_t *s_k0) {
-    static_assert(3 * K <= 64, "one lane per (quantity, scale)");
+    static_assert(4 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
     const int H = c.H, J = c.J;
@@ -1835,13 +1835,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     if (lane == 0) c.scale[e] = total;  // ablation: row setup only
     return;
 #endif
-    const int grp = lane / K < 2 ? lane / K : 2;  // lanes past 3K: a spare copy of group 2
+    // lane g*K + kk: quantity g of scale kk, g = 0..3 (L, L cos, L sin, and the
+    // contributor count as a sum of 1.0: exact); lanes past 4K fold junk
+    const int grp = lane / K < 3 ? lane / K : 3;
     const int kk = lane - grp * K;
+    s_val[4 * lane + 3] = 1.0;  // the count's "value" in every staging slot (staging never overwrites it)
     const uint64_t lt = (1ull << lane) - 1;
     double acc = 0.0;
-    int cntk[K];  // wave-uniform
-#pragma unroll
-    for (int k = 0; k < K; ++k) cntk[k] = 0;
     int ncon_total = 0;
     // lanes without a contributor load the event's own flow (a valid address,
     // finite values that a non-member fold adds as +0)
@@ -1905,15 +1905,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         if (pbal) {
             const int cnt = (int)__popcll(pbal);
             const bool pc = (pbal >> lane) & 1;
-#pragma unroll
-            for (int k = 0; k < K; ++k) cntk[k] += (int)__popcll(__ballot(pc && pk0 <= k));
             // every lane writes one slot: contributors [0, cnt) in rank order,
             // the others after them with k0 = K (in no scale)
             const int slot = pc ? (int)__popcll(pbal & lt) : cnt + (int)__popcll(~pbal & lt);
             // the previous fold's LDS reads are done (wave-private LDS)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            s_val[3 * slot] = p0; s_val[3 * slot + 1] = p1; s_val[3 * slot + 2] = p2;
+            s_val[4 * slot] = p0; s_val[4 * slot + 1] = p1; s_val[4 * slot + 2] = p2;
             s_k0[slot] = (uint8_t)(pc ? pk0 : K);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1932,13 +1930,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 #if FARMS_POOL_FOLD_ASM
                 double v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = s_val[3 * (r + u) + grp];
+                for (int u = 0; u < 8; ++u) v[u] = s_val[4 * (r + u) + grp];
                 fold8(acc, kk, kw[0], kw[1], v);
 #else
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
                     const int k0u = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
-                    const double v = s_val[3 * (r + u) + grp];
+                    const double v = s_val[4 * (r + u) + grp];
                     const double m = kk >= k0u ? 1.0 : 0.0;
                     acc = __builtin_fma(v, m, acc);
                 }
@@ -1954,23 +1952,18 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     }
     // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
     // the winner is the lowest k whose mean equals the maximum, if it is > 0
-    int cnt_kk = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) cnt_kk = kk == k ? cntk[k] : cnt_kk;
+    const double cnt_kk = __shfl(acc, 3 * K + (lane < K ? lane : 0), 64);  // contributors of scale lane
     const bool is_len = lane < K;
-    const double mean = is_len && cnt_kk > 0 ? acc / (double)cnt_kk : 0.0;
+    const double mean = is_len && cnt_kk > 0 ? acc / cnt_kk : 0.0;
     const double maxv = wave_max(mean);
     const int mi = maxv > 0 ? __builtin_ctzll(__ballot(is_len && mean == maxv)) : 0;
-    const double sx = __shfl(acc, K + mi, 64), sy = __shfl(acc, 2 * K + mi, 64);
+    const double sx = __shfl(acc, K + mi, 64), sy = __shfl(acc, 2 * K + mi, 64), cnt_mi = __shfl(acc, 3 * K + mi, 64);
     if (lane == 0) {
         double gx, gy;
         int sc;
         if (maxv > 0) {
-            int cnt_mi = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) cnt_mi = mi == k ? cntk[k] : cnt_mi;
-            gx = sx / (double)cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
-            gy = sy / (double)cnt_mi;
+            gx = sx / cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
+            gy = sy / cnt_mi;
             sc = mi * J;
         } else {  // vFlow.cpp:1085-1094
             const FlowCell self = c.evf[e];
@@ -2004,6 +1997,9 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #ifndef FARMS_POOL_VGPR_FLOOR
 #define FARMS_POOL_VGPR_FLOOR "v79"  // k_pool occupancy cap (see k_pool)
 #endif
+#ifndef FARMS_POOL_EPW
+#define FARMS_POOL_EPW 1  // work-order positions per pooling wave
+#endif
 #ifndef FARMS_POOL_WPB
 #define FARMS_POOL_WPB 1  // waves (events) per k_pool workgroup: one, so that a finished event frees its slot at once
 #endif
@@ -2015,30 +2011,33 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int w = c0 + work_block() * FARMS_POOL_WPB + wv;
-    if (w >= c1) return;
-    const int e = c.Q[w];
-    // the event's fields load together with its validity flag
-    const uint32_t vld = c.valid[e];
-    const int ex = c.x[e], ey = c.y[e];
-    const uint32_t teu = c.t[e];
-    // keep the compiler from sinking the field loads below the exits: the four
-    // loads then share one round trip
-    asm volatile("" ::"v"(vld), "v"(ex), "v"(ey), "v"(teu));
-    if (!vld) return;
-    if (ex < c.own_lo || ex >= c.own_hi) return;
     // Occupancy cap: the kernel allocates at least 80 VGPRs, i.e. at most 6
     // pooling waves per SIMD (70 would allow 7).  The fit sweep's waves need
     // the room: each of its 1,500 launches per C3 step waits for its slowest
     // wave, so crowding them stretches the whole pipeline (measured at C3:
     // 6 waves/SIMD 109.9 ms per step, 7: 122.0, 5: 113.9).
     asm volatile("" ::: FARMS_POOL_VGPR_FLOOR);
-    const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
     uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolValWords);
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
-    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * 64);
-    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64);
+    // FARMS_POOL_EPW consecutive work-order positions per wave (one chunk: C2
+    // is a multiple of it)
+    const int w0 = c0 + (work_block() * FARMS_POOL_WPB + wv) * FARMS_POOL_EPW;
+#pragma unroll 1
+    for (int w = w0; w < w0 + FARMS_POOL_EPW && w < c1; ++w) {
+        const int e = c.Q[w];
+        // the event's fields load together with its validity flag
+        const uint32_t vld = c.valid[e];
+        const int ex = c.x[e], ey = c.y[e];
+        const uint32_t teu = c.t[e];
+        // keep the compiler from sinking the field loads below the exits: the
+        // four loads then share one round trip
+        asm volatile("" ::"v"(vld), "v"(ex), "v"(ey), "v"(teu));
+        if (!vld || ex < c.own_lo || ex >= c.own_hi) continue;
+        const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
+        pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
+    }
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -2321,7 +2320,8 @@ template <int K>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
     const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
-    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, FARMS_POOL_WPB)), dim3(64 * FARMS_POOL_WPB), lds, s, c, c0, c1);
+    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, FARMS_POOL_WPB * FARMS_POOL_EPW)), dim3(64 * FARMS_POOL_WPB), lds, s,
+                       c, c0, c1);
 }
 
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);

@@ -166,6 +166,7 @@ struct Ctx {
     const uint32_t *skey;  // pixel ids, sorted
     const int32_t *P;      // event ids sorted by (pixel, id)
     const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
+    int4 *qe;              // per work-order position: {event id or -1 if not pooled, x, y, t} (k_pool_desc)
     // per event, one 16-B record (k_link): {position in P, previous and next
     // event at the pixel (-1 / INT_MAX: none), tpv}; tpv = the stamp the
     // pixel's SAE holds just before the event (the previous event's, or, for
@@ -398,6 +399,20 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, in
         }
     }
     if (nx >= c1) cells[q].run_hi = lk.x;
+}
+
+// Pooling descriptors of work-order positions [p0, p1): {event, x, y, t}, the
+// event -1 when it is not pooled here (invalid flow, or a halo event its owner
+// pools), so that a pooling wave needs one load where it needed two dependent
+// round trips (Q, then the event's fields).  Runs after the fits of the
+// positions' chunks.
+__global__ void k_pool_desc(Ctx c, int p0, int p1) {
+    const int w = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (w >= p1) return;
+    const int e = c.Q[w];
+    const int ex = c.x[e], ey = c.y[e];
+    const bool ok = c.valid[e] && ex >= c.own_lo && ex < c.own_hi;
+    c.qe[w] = make_int4(ok ? e : -1, ex, ey, (int)c.t[e]);
 }
 
 // The prep of one fit chunk as its own launch (the first chunk of a call, the
@@ -1453,10 +1468,13 @@ __device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
     const FlowCell f = *p;
     return ChainFlow{f.L, f.Lc, f.Ls, f.t};
 }
-__global__ __launch_bounds__(256, 4) void k_chain(Ctx c, int ch0, int ch1) {
+#ifndef FARMS_CHAIN_WPB
+#define FARMS_CHAIN_WPB 1  // waves per k_chain workgroup (the waves are independent)
+#endif
+__global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, 4) void k_chain(Ctx c, int ch0, int ch1) {
     if (FARMS_CHAIN_PRIO) __builtin_amdgcn_s_setprio(FARMS_CHAIN_PRIO);
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t g = (int64_t)blockIdx.x * FARMS_CHAIN_WPB + (threadIdx.x >> 6);
     if (g >= c.nblk) return;
     const int n = c.n, C2 = c.C2;
     const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
@@ -2026,15 +2044,11 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     const int w0 = c0 + (work_block() * FARMS_POOL_WPB + wv) * FARMS_POOL_EPW;
 #pragma unroll 1
     for (int w = w0; w < w0 + FARMS_POOL_EPW && w < c1; ++w) {
-        const int e = c.Q[w];
-        // the event's fields load together with its validity flag
-        const uint32_t vld = c.valid[e];
-        const int ex = c.x[e], ey = c.y[e];
-        const uint32_t teu = c.t[e];
-        // keep the compiler from sinking the field loads below the exits: the
-        // four loads then share one round trip
-        asm volatile("" ::"v"(vld), "v"(ex), "v"(ey), "v"(teu));
-        if (!vld || ex < c.own_lo || ex >= c.own_hi) continue;
+        // the event and its fields in one 16-B load (k_pool_desc)
+        const int4 d = c.qe[w];
+        if (d.x < 0) continue;  // invalid flow, or a halo event (pooled by its owner)
+        const int e = d.x, ex = d.y, ey = d.z;
+        const uint32_t teu = (uint32_t)d.w;
         const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
         pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
     }
@@ -2206,6 +2220,7 @@ struct farms_handle {
     int32_t *iota = nullptr, *P = nullptr;
     int4 *link = nullptr;
     int32_t *Q = nullptr;
+    int4 *qe = nullptr;
     // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
     const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
     const uint32_t *ph_t = nullptr;
@@ -2258,7 +2273,7 @@ void dfree(T *&p) {
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->link);
-    dfree(h->Q); dfree(h->wkey); dfree(h->wkey_sorted);
+    dfree(h->Q); dfree(h->qe); dfree(h->wkey); dfree(h->wkey_sorted);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2281,7 +2296,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
     if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
         (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
         (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->link, cap)) ||
-        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
+        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->qe, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
         (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
@@ -2406,7 +2421,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.link = h->link;
-    c.Q = h->Q;
+    c.Q = h->Q; c.qe = h->qe;
     c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.pcur = h->pcur; c.pend = h->pend;
@@ -2573,7 +2588,11 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             const int fl = std::min(f, n_fit_chunks - 1);
             if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
-        hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, 4)), dim3(256), 0, sc, c, ch0, ch1);
+        hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, FARMS_CHAIN_WPB)), dim3(64 * FARMS_CHAIN_WPB), 0, sc, c, ch0, ch1);
+        {
+            const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
+            hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
+        }
         HIPCHK(hipEventRecord(ev_cand(S), sc));
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);

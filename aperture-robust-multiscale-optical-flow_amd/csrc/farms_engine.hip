@@ -147,7 +147,11 @@ constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 // valid while candidate slots stay below 2^24 (W * H <= kMaxSlots)
 constexpr int kRowBias = 1 << 14;  // flattened positions of a window < 128 x 128
 constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
-constexpr int kPoolValWords = 4 * 64 + 8;  // k_pool staging: {L, L cos, L sin, 1} and k0 of 64 entries, 8-B words
+#ifndef FARMS_POOL_HALVES
+#define FARMS_POOL_HALVES 1  // candidates per lane per pooling step (1 or 2)
+#endif
+// k_pool staging: {L, L cos, L sin, 1} and k0 of the 64 x FARMS_POOL_HALVES entries of a step, 8-B words
+constexpr int kPoolValWords = (4 * 64 + 8) * FARMS_POOL_HALVES;
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -1732,7 +1736,7 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
     // bit of s_start, and its candidate offset in s_row
     uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
     {
-        const int nw = (nrows * (j_hi - j_lo + 1) + 63) >> 6;  // bound on the flattened length, in words
+        const int nw = ((nrows * (j_hi - j_lo + 1) + 63) >> 6) + 1;  // bound on the flattened length, in words (+1)
         for (int i = lane; i < nw; i += 64) s_start[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1857,116 +1861,158 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     // contributor count as a sum of 1.0: exact); lanes past 4K fold junk
     const int grp = lane / K < 3 ? lane / K : 3;
     const int kk = lane - grp * K;
-    s_val[4 * lane + 3] = 1.0;  // the count's "value" in every staging slot (staging never overwrites it)
+    constexpr int NH = FARMS_POOL_HALVES;  // candidates per lane per step: a step covers 64 * NH positions
+#pragma unroll
+    for (int h = 0; h < NH; ++h) s_val[4 * (lane + 64 * h) + 3] = 1.0;  // the count's "value" (staging never overwrites it)
     const uint64_t lt = (1ull << lane) - 1;
     double acc = 0.0;
     int ncon_total = 0;
     // lanes without a contributor load the event's own flow (a valid address,
     // finite values that a non-member fold adds as +0)
     const double *const vdummy = reinterpret_cast<const double *>(c.evf + e);
-    // Flattened positions [f0, f0 + 64) per step: lane f's segment is the last
-    // non-empty one starting at or before f, i.e. the (number of segment
-    // starts <= f)-th one.
+    // Flattened position f = f0 + 64 h + lane: its segment is the last non-empty
+    // one starting at or before f, i.e. the (number of segment starts <= f)-th.
     int mbase = 0;
-    auto locate = [&](int f0, int &row, int &k) {
-        const uint64_t mk = s_start[f0 >> 6];
-        const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
-        mbase += (int)__popcll(mk);
-        const uint32_t rs = s_row[m < 0 ? 0 : m];
-        row = (int)(rs >> 25);
-        k = f0 + lane + (int)(rs & 0x1FFFFFFu) - kRowBias;
-    };
-    int rc = 0, kc = 0;
-    CandHdr hc{};
-    if (total > 0) { locate(0, rc, kc); if (lane < total) hc = chdr[kc]; }
-    // the previous step's contributors: ballot, values, smallest scale
-    uint64_t pbal = 0;
-    double p0 = 0.0, p1 = 0.0, p2 = 0.0;
-    int pk0 = K;
-    for (int f0 = 0;; f0 += 64) {
-        const bool have = f0 < total;  // wave-uniform
-        bool con = false;
-        int k0 = K;
-        const double *vp = vdummy;
-        if (have && f0 + lane < total) {
-            uint32_t tq;
-            bool ok;
-            if (hc.e1 > e) { ok = (hc.lin & kCandSnapOk) != 0; tq = hc.t_snap; vp = &cval[kc].L_snap; }
-            else if (!(hc.lin & kCandMore)) { ok = (hc.lin & kCandOneOk) != 0; tq = hc.t1; vp = &cval[kc].L1; }
-            else {  // several events at the cell inside the chunk: search its run
-                const CandVal &cv = cval[kc];
-                const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
-                const FlowCell fe = c.evf[sev];
-                ok = fe.L > 0; tq = fe.t; vp = &c.evf[sev].L;
-            }
-            if ((hc.lin & kCandLinMask) == own_lin) tq = own_tprev;
-            // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
-            const int64_t dt = (int64_t)teu - (int64_t)tq;
-            const int i = row_i0 + rc;
-            const int j = (int)(hc.lin & kCandLinMask) + OFF - i * H;
-            if (ok && (uint64_t)(dt + 499) < 999u) {
-                const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
-                const int d = di > dj ? di : dj;
-                k0 = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);  // smallest scale containing the cell: ceil(d / J)
-                con = true;
-            }
+    auto locate = [&](int f0, int (&row)[NH], int (&k)[NH]) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const uint64_t mk = s_start[(f0 >> 6) + h];
+            const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
+            mbase += (int)__popcll(mk);
+            const uint32_t rs = s_row[m < 0 ? 0 : m];
+            row[h] = (int)(rs >> 25);
+            k[h] = f0 + 64 * h + lane + (int)(rs & 0x1FFFFFFu) - kRowBias;
         }
-        if (!con) vp = vdummy;
+    };
+    int rc[NH], kc[NH];
+    CandHdr hc[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) { rc[h] = 0; kc[h] = 0; hc[h] = CandHdr{}; }
+    if (total > 0) {
+        locate(0, rc, kc);
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            if (64 * h + lane < total) hc[h] = chdr[kc[h]];
+    }
+    // the previous step's contributors: ballots, values, smallest scales
+    uint64_t pbal[NH];
+    double pv[NH][3];
+    int pk0[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) { pbal[h] = 0; pv[h][0] = pv[h][1] = pv[h][2] = 0.0; pk0[h] = K; }
+    for (int f0 = 0;; f0 += 64 * NH) {
+        const bool have = f0 < total;  // wave-uniform
+        bool con[NH];
+        int k0[NH];
+        const double *vp[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            con[h] = false;
+            k0[h] = K;
+            vp[h] = vdummy;
+            if (have && f0 + 64 * h + lane < total) {
+                const CandHdr &hd = hc[h];
+                uint32_t tq;
+                bool ok;
+                if (hd.e1 > e) { ok = (hd.lin & kCandSnapOk) != 0; tq = hd.t_snap; vp[h] = &cval[kc[h]].L_snap; }
+                else if (!(hd.lin & kCandMore)) { ok = (hd.lin & kCandOneOk) != 0; tq = hd.t1; vp[h] = &cval[kc[h]].L1; }
+                else {  // several events at the cell inside the chunk: search its run
+                    const CandVal &cv = cval[kc[h]];
+                    const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
+                    const FlowCell fe = c.evf[sev];
+                    ok = fe.L > 0; tq = fe.t; vp[h] = &c.evf[sev].L;
+                }
+                if ((hd.lin & kCandLinMask) == own_lin) tq = own_tprev;
+                // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
+                const int64_t dt = (int64_t)teu - (int64_t)tq;
+                const int i = row_i0 + rc[h];
+                const int j = (int)(hd.lin & kCandLinMask) + OFF - i * H;
+                if (ok && (uint64_t)(dt + 499) < 999u) {
+                    const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
+                    const int d = di > dj ? di : dj;
+                    k0[h] = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);  // smallest scale containing the cell: ceil(d / J)
+                    con[h] = true;
+                }
+            }
+            if (!con[h]) vp[h] = vdummy;
+        }
         // this step's values and the next step's headers: both in flight during
         // the fold below (unconditional loads: a load under a branch would be
         // waited for at the branch end)
-        const double v0 = vp[0], v1 = vp[1], v2 = vp[2];
-        int rn = 0, kn = 0;
-        CandHdr hn{};
-        if (f0 + 64 < total) { locate(f0 + 64, rn, kn); if (f0 + 64 + lane < total) hn = chdr[kn]; }
+        double v[NH][3];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) { v[h][0] = vp[h][0]; v[h][1] = vp[h][1]; v[h][2] = vp[h][2]; }
+        int rn[NH], kn[NH];
+        CandHdr hn[NH];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) { rn[h] = 0; kn[h] = 0; hn[h] = CandHdr{}; }
+        if (f0 + 64 * NH < total) {
+            locate(f0 + 64 * NH, rn, kn);
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+                if (f0 + 64 * (NH + h) + lane < total) hn[h] = chdr[kn[h]];
+        }
         // ---- stage and fold the previous step's contributors
-        if (pbal) {
-            const int cnt = (int)__popcll(pbal);
-            const bool pc = (pbal >> lane) & 1;
-            // every lane writes one slot: contributors [0, cnt) in rank order,
-            // the others after them with k0 = K (in no scale)
-            const int slot = pc ? (int)__popcll(pbal & lt) : cnt + (int)__popcll(~pbal & lt);
+        uint64_t pany = 0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) pany |= pbal[h];
+        if (pany) {
+            // every lane writes one slot per half: the contributors first, in
+            // raster order (half 0 before half 1), then the others with k0 = K
+            // (in no scale)
+            int cntb[NH], cnt = 0;
+#pragma unroll
+            for (int h = 0; h < NH; ++h) { cntb[h] = (int)__popcll(pbal[h]); cnt += cntb[h]; }
             // the previous fold's LDS reads are done (wave-private LDS)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            s_val[4 * slot] = p0; s_val[4 * slot + 1] = p1; s_val[4 * slot + 2] = p2;
-            s_k0[slot] = (uint8_t)(pc ? pk0 : K);
+            int cbase = 0, nbase = cnt;
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const bool pc = (pbal[h] >> lane) & 1;
+                const int slot = pc ? cbase + (int)__popcll(pbal[h] & lt) : nbase + (int)__popcll(~pbal[h] & lt);
+                s_val[4 * slot] = pv[h][0]; s_val[4 * slot + 1] = pv[h][1]; s_val[4 * slot + 2] = pv[h][2];
+                s_k0[slot] = (uint8_t)(pc ? pk0[h] : K);
+                cbase += cntb[h];
+                nbase += 64 - cntb[h];
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
-            // Member entries are added as fma(v, 1, acc) = acc + v (one
-            // rounding), non-members as fma(v, 0, acc) = acc + (+-0) = acc: acc
-            // starts at +0 and a round-to-nearest sum is -0 only when both
-            // addends are, so acc is never -0 and the masked fold is bitwise
-            // the reference's conditional one (valid flows are finite).  The
-            // multiplier is off the dependency chain: one fma per entry on it.
 #pragma unroll 1
             for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // slots past cnt: k0 = K
                 uint32_t kw[FARMS_POOL_UNROLL / 4];
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL / 4; ++u) kw[u] = k4p[(r >> 2) + u];
 #if FARMS_POOL_FOLD_ASM
-                double v[8];
+                double vv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = s_val[4 * (r + u) + grp];
-                fold8(acc, kk, kw[0], kw[1], v);
+                for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
+                fold8(acc, kk, kw[0], kw[1], vv);
 #else
+                // members as fma(v, 1, acc) = acc + v, non-members as fma(v, 0,
+                // acc) = acc + (+-0) = acc: acc starts at +0 and a round-to-
+                // nearest sum is -0 only when both addends are, so this is
+                // bitwise the conditional add (valid flows are finite)
 #pragma unroll
                 for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
                     const int k0u = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
-                    const double v = s_val[4 * (r + u) + grp];
+                    const double vu = s_val[4 * (r + u) + grp];
                     const double m = kk >= k0u ? 1.0 : 0.0;
-                    acc = __builtin_fma(v, m, acc);
+                    acc = __builtin_fma(vu, m, acc);
                 }
 #endif
             }
             ncon_total += cnt;
         }
         if (!have) break;
-        pbal = __ballot(con);
-        p0 = v0; p1 = v1; p2 = v2;
-        pk0 = k0;
-        hc = hn; rc = rn; kc = kn;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            pbal[h] = __ballot(con[h]);
+            pv[h][0] = v[h][0]; pv[h][1] = v[h][1]; pv[h][2] = v[h][2];
+            pk0[h] = k0[h];
+            hc[h] = hn[h]; rc[h] = rn[h]; kc[h] = kn[h];
+        }
     }
     // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
     // the winner is the lowest k whose mean equals the maximum, if it is > 0
@@ -2038,7 +2084,7 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolValWords);
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
-    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64 * FARMS_POOL_HALVES);
     // FARMS_POOL_EPW consecutive work-order positions per wave (one chunk: C2
     // is a multiple of it)
     const int w0 = c0 + (work_block() * FARMS_POOL_WPB + wv) * FARMS_POOL_EPW;
@@ -2430,7 +2476,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     const int span = 2 * h->M + 1;  // pooling window rows and columns
-    c.pool_bw = (span * span + 63) / 64;  // flattened window positions
+    c.pool_bw = (span * span + 63) / 64 + 1;  // flattened window positions (+1: a two-half step reads a word ahead)
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
     c.r_local = dout->r_local; c.th_local = dout->theta_local; c.scale = dout->scale;

@@ -839,6 +839,13 @@ __device__ __forceinline__ int xch32(int v) {
     else if constexpr (S == 4) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
     else return __shfl_xor(v, 32, 64);
 }
+// lane U of the quad, to every lane of the quad (DPP quad_perm [U,U,U,U])
+template <int U>
+__device__ __forceinline__ double quad_bcast(double v) {
+    constexpr int ctl = U | (U << 2) | (U << 4) | (U << 6);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), ctl, 0xF, 0xF, true),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), ctl, 0xF, 0xF, true));
+}
 template <int S>
 __device__ __forceinline__ double xch(double v) {
     return __hiloint2double(xch32<S>(__double2hiint(v)), xch32<S>(__double2loint(v)));
@@ -1164,37 +1171,43 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
     DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
     const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
     const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
-    const double d2 = DET * (a[5] * a[1] - a[4] * a[2]);
     const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
     const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
-    const double d5 = DET * (a[3] * a[2] - a[5] * a[0]);
-    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);  // (d2, d5, d8: the intercept row, never used)
     const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
-    const double d8 = DET * (a[4] * a[0] - a[3] * a[1]);
     constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
     const double cz = (double)te * kTsToSec;
-    double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+    // (A2 * At) * Y in the reference order (r2, the intercept, is never used:
+    // vFlow.cpp:1352-1377).  Each term m_k * yt_k is one rounded product,
+    // independent of the others, so lane j of the quad forms the terms of
+    // cells k = kb + j, and the sums then add them in order k = 0, 1, ... on
+    // every lane (quad broadcasts): the additions are the reference's, a quarter
+    // of the products per lane.
+    double r0 = 0.0, r1 = 0.0;
 #pragma unroll 1
-    for (int k = 0; k < np; ++k) {  // every lane, reference order
+    for (int kb = 0; kb < np; kb += 4) {
+        const int k = kb + j < np ? kb + j : np - 1;
         int64_t Xi, Yi; uint32_t T;
         cell(k, Xi, Yi, T);
         const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
         const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-        double m0, m1, m2;
+        double m0, m1;
         if (gemm) {
             m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
             m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
-            m2 = (((0.0 + d2 * X) + d5 * Y) + d8 * 1.0) + 0.0;
         } else {
             m0 = (d0 * X + d3 * Y) + d6 * 1.0;
             m1 = (d1 * X + d4 * Y) + d7 * 1.0;
-            m2 = (d2 * X + d5 * Y) + d8 * 1.0;
         }
-        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; r2 = m2 * yt; }
-        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; r2 = r2 + m2 * yt; }
+        const double q0 = m0 * yt, q1 = m1 * yt;
+        const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
+        if (!gemv && kb == 0) { r0 = a0; r1 = a1; }
+        else { r0 = r0 + a0; r1 = r1 + a1; }
+        if (kb + 1 < np) { r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1); }
+        if (kb + 2 < np) { r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1); }
+        if (kb + 3 < np) { r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1); }
     }
-    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; r2 = r2 + 0.0; }
-    (void)r2;
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
     const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
     const double ccx = (double)ex, ccy = (double)ey;
     int inliers = 0;

@@ -1488,7 +1488,10 @@ __device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
 #ifndef FARMS_CHAIN_WPB
 #define FARMS_CHAIN_WPB 1  // waves per k_chain workgroup (the waves are independent)
 #endif
-__global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, 4) void k_chain(Ctx c, int ch0, int ch1) {
+#ifndef FARMS_CHAIN_WAVES
+#define FARMS_CHAIN_WAVES 4  // k_chain waves per SIMD the register allocation must allow
+#endif
+__global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0, int ch1) {
     if (FARMS_CHAIN_PRIO) __builtin_amdgcn_s_setprio(FARMS_CHAIN_PRIO);
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x * FARMS_CHAIN_WPB + (threadIdx.x >> 6);

@@ -1527,18 +1527,20 @@ __global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_cha
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) prefetch(i);
     // the chunks' stamp spans, lane l holding chunk ch0 + l (read with a
-    // wave-uniform readlane: no memory round trip per chunk)
-    const bool spans_in_regs = ch1 - ch0 <= 64;
-    const uint32_t tmin_l = (spans_in_regs && ch0 + lane < ch1) ? c.ctmin[ch0 + lane] : 0u;
-    const uint32_t tmax_l = (spans_in_regs && ch0 + lane < ch1) ? c.ctmax[ch0 + lane] : 0u;
-    // wait for them here, once: otherwise the loop header waits for every
-    // outstanding load (the prefetches included) before each readlane
+    // wave-uniform readlane: no memory round trip per chunk; a launch covers
+    // at most 64 chunks).  Unconditional loads from a clamped index: a
+    // conditional one merged into the same register would make every readlane
+    // wait for all outstanding loads, the prefetches included.
+    const int chl = min(ch0 + lane, ch1 - 1);
+    const uint32_t tmin_l = c.ctmin[chl];
+    const uint32_t tmax_l = c.ctmax[chl];
+    // wait for them here, once
     asm volatile("" ::"v"(tmin_l), "v"(tmax_l));
     for (int ch = ch0; ch < ch1; ++ch) {
         const int b = ch % c.NB;
         const int ce = min((ch + 1) * C2, n);
-        const uint32_t tmin = spans_in_regs ? (uint32_t)__builtin_amdgcn_readlane((int)tmin_l, ch - ch0) : c.ctmin[ch];
-        const uint32_t tmax = spans_in_regs ? (uint32_t)__builtin_amdgcn_readlane((int)tmax_l, ch - ch0) : c.ctmax[ch];
+        const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)tmin_l, ch - ch0);
+        const uint32_t tmax = (uint32_t)__builtin_amdgcn_readlane((int)tmax_l, ch - ch0);
         const int64_t lo = (int64_t)tmin - (int64_t)kKillUs, hi = (int64_t)tmax + (int64_t)kKillUs;
         uint64_t bal[kChainCells];
         uint32_t woff[kChainCells];
@@ -2650,7 +2652,9 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             const int fl = std::min(f, n_fit_chunks - 1);
             if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
-        hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, FARMS_CHAIN_WPB)), dim3(64 * FARMS_CHAIN_WPB), 0, sc, c, ch0, ch1);
+        for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
+            hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, FARMS_CHAIN_WPB)), dim3(64 * FARMS_CHAIN_WPB), 0, sc, c, a,
+                               std::min(a + 64, ch1));
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);

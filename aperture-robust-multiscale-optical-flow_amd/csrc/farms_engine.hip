@@ -182,6 +182,7 @@ struct Ctx {
     FlowCell *fsnap;       // flow snapshot
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
     FlowCell *evf;         // per-event local flow
+    double2 *plane;        // per event: the fitted plane's slopes (a, b), from the fit to k_flow
     uint8_t *valid;
     int32_t *pcur, *pend;  // pooling sweep, per cell: cursor into the cell's run of P, last run position (-1: none)
     // ring of NB per-chunk candidate buffers (chunk ch uses buffer ch % NB):
@@ -479,7 +480,7 @@ __device__ __forceinline__ double det3_partialpivlu(const double a[9]) {
 // Local plane fit of one event (computeLocalFlow + computeGrads, vFlow.cpp:
 // 863-942, 1290-1380) for any fRad, every lookup complete, one thread.  Used
 // for very large filters only (k_fit_wave stages smaller ones in LDS).
-__device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_out, double &vy_out) {
+__device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_out, double &vy_out, bool &acc_out) {
     const int fr = c.fr;
     const int side = 2 * fr + 1;
     const int np = side * side;
@@ -488,6 +489,7 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
     const uint32_t te = c.t[e];
     vx_out = 0.0;
     vy_out = 0.0;
+    acc_out = false;
     // ---- window scores (vFlow.cpp:870-912): sum over the window of
     // (t_e - t_k) + 2^32 [t_k > t_e], exact as int64; ties: first strict min.
     bool wok[9];
@@ -592,12 +594,10 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
         if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    const double speed = 1.0 / dtdp;
-    const double angle = F_ATAN2(r0, r1);
-    double sn_, cs_;
-    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
-    vx_out = speed * cs_;
-    vy_out = speed * sn_;
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
 }
 
 // Local plane fit of one event with fRad known at compile time (the common
@@ -610,13 +610,14 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
 // three passes over it.  Arithmetic is that of fit_event_generic.
 template <int FR>
 __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq, uint32_t *lt, double &vx_out,
-                                               double &vy_out) {
+                                               double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
     const int ex = c.x[e], ey = c.y[e];
     const uint32_t te = c.t[e];
     vx_out = 0.0;
     vy_out = 0.0;
+    acc_out = false;
     bool wok[9];
     int64_t score[9];
     bool any = false;
@@ -769,12 +770,10 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq
         if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
     }
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    const double speed = 1.0 / dtdp;
-    const double angle = F_ATAN2(r0, r1);
-    double sn_, cs_;
-    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
-    vx_out = speed * cs_;
-    vy_out = speed * sn_;
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
 }
 
 // Validity gate, flow-surface value and record of one fitted event.
@@ -808,6 +807,43 @@ __device__ __forceinline__ void fit_store(const Ctx &c, int e, double vx, double
     if (c.ox) { c.ox[e] = ex; c.oy[e] = ey; c.ot[e] = (int32_t)te; c.op[e] = c.p[e]; }
 }
 
+// The fit kernels end at the plane: its slopes (a, b) and whether the window
+// search, the determinant and the inlier count accepted it (in c.valid until
+// k_flow writes the validity there).  The libm chain that turns them into the
+// local flow runs in k_flow, one lane per event, instead of on a quad's four
+// lanes (or one of them) inside the fit.
+__device__ __forceinline__ void fit_plane(const Ctx &c, int e, double r0, double r1, bool acc) {
+    c.plane[e] = make_double2(r0, r1);
+    c.valid[e] = acc ? 1 : 0;
+}
+
+// Local flow of events [e0, e1) from their planes (vFlow.cpp:1349-1377, then
+// the validity gate and flow-surface value, fit_store): speed = 1 / |(a, b)|,
+// angle = atan2(a, b), (Vx, Vy) = speed (cos, sin)(angle); (0, 0) when the plane
+// was rejected.  Halo events of an x-strip (not fitted here) are left to
+// farms_import_flows.
+__global__ void k_flow(Ctx c, int e0, int e1) {
+    const int e = e0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (e >= e1) return;
+    if (!c.fit_all) {
+        const int ex = c.x[e];
+        if (ex < c.fit_lo || ex >= c.fit_hi) return;
+    }
+    double vx = 0.0, vy = 0.0;
+    if (c.valid[e]) {
+        const double2 pl = c.plane[e];
+        const double r0 = pl.x, r1 = pl.y;
+        const double dtdp = sqrt(r0 * r0 + r1 * r1);  // pow(v, 2.0) as v*v
+        const double speed = 1.0 / dtdp;
+        const double angle = F_ATAN2(r0, r1);
+        double sn_, cs_;
+        F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
+        vx = speed * cs_;
+        vy = speed * sn_;
+    }
+    fit_store(c, e, vx, vy);
+}
+
 // One thread per event of chunk [c0, c1) in tile order.
 template <int FR>
 __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq) {
@@ -821,8 +857,9 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
         if (ex < c.fit_lo || ex >= c.fit_hi) return;
     }
     double vx, vy;
-    fit_event_fast<FR>(c, e, seq, s_tk + threadIdx.x, vx, vy);
-    fit_store(c, e, vx, vy);
+    bool acc;
+    fit_event_fast<FR>(c, e, seq, s_tk + threadIdx.x, vx, vy, acc);
+    fit_plane(c, e, vx, vy, acc);
 }
 
 
@@ -883,13 +920,14 @@ constexpr int kFitQS = 16 * FARMS_FIT_WPB;  // quads per fit workgroup: stride o
 
 template <int FR>
 __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq, int j, uint32_t *lt, double &vx_out,
-                                               double &vy_out) {
+                                               double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
     const int ex = c.x[e], ey = c.y[e];
     const uint32_t te = c.t[e];
     vx_out = 0.0;
     vy_out = 0.0;
+    acc_out = false;
     bool wok[9];
     int64_t score[9];
     bool any = false;
@@ -1042,12 +1080,10 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
     inliers += xch32<0>(inliers);
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    const double speed = 1.0 / dtdp;
-    const double angle = F_ATAN2(r0, r1);
-    double sn_, cs_;
-    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
-    vx_out = speed * cs_;
-    vy_out = speed * sn_;
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
 }
 
 // Variant that keeps the union: every lane writes the stamps of its union
@@ -1056,13 +1092,14 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
 // round of loads (window column cxo is union column (bw / 3) * FR + cxo).
 template <int FR>
 __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t seq, int j, uint32_t *ut, double &vx_out,
-                                                 double &vy_out) {
+                                                 double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
     const int ex = c.x[e], ey = c.y[e];
     const uint32_t te = c.t[e];
     vx_out = 0.0;
     vy_out = 0.0;
+    acc_out = false;
     bool wok[9];
     int64_t score[9];
     bool any = false;
@@ -1224,12 +1261,10 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
     inliers += xch32<0>(inliers);
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    const double speed = 1.0 / dtdp;
-    const double angle = F_ATAN2(r0, r1);
-    double sn_, cs_;
-    F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
-    vx_out = speed * cs_;
-    vy_out = speed * sn_;
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
 }
 
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
@@ -1262,9 +1297,10 @@ __global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_qua
         if (ex < c.fit_lo || ex >= c.fit_hi) return;  // the whole quad
     }
     double vx, vy;
-    if constexpr (UT) fit_event_quad_u<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
-    else fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy);
-    if (j == 0) fit_store(c, e, vx, vy);
+    bool acc;
+    if constexpr (UT) fit_event_quad_u<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    else fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    if (j == 0) fit_plane(c, e, vx, vy, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1291,8 +1327,9 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
     if (nU > kFitWaveCap) {  // very large filters: per-thread path on lane 0
         if (lane == 0) {
             double vx, vy;
-            fit_event_generic(c, e, seq, vx, vy);
-            fit_store(c, e, vx, vy);
+            bool acc;
+            fit_event_generic(c, e, seq, vx, vy, acc);
+            fit_plane(c, e, vx, vy, acc);
         }
         return;
     }
@@ -1305,7 +1342,7 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
         any |= wok[w];
     }
     if (!any) {
-        if (lane == 0) fit_store(c, e, 0.0, 0.0);
+        if (lane == 0) fit_plane(c, e, 0.0, 0.0, false);
         return;
     }
     // ---- stage the union window and score the 9 windows (vFlow.cpp:870-912)
@@ -1341,7 +1378,7 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
         if (wok[w] && sw < best) { best = sw; bw = w; }
     }
     if (bw < 0 || best > nn * (int64_t(1) << 32)) {
-        if (lane == 0) fit_store(c, e, 0.0, 0.0);
+        if (lane == 0) fit_plane(c, e, 0.0, 0.0, false);
         return;
     }
     // ---- the winning window, cx-major (vFlow.cpp:923-930)
@@ -1415,17 +1452,12 @@ __device__ void fit_wave_event(const Ctx &c, int e, uint32_t seq, uint32_t *s_t,
             if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inl;
         }
         inliers = (int)wave_sum_i64(inl);
-        const double speed = 1.0 / dtdp;
-        const double angle = F_ATAN2(r0, r1);
-        double sn_, cs_;
-        F_SINCOS(angle, &sn_, &cs_);  // one range reduction for both
-        dtdx = speed * cs_;
-        dtdy = speed * sn_;
+        dtdx = r0;
+        dtdy = r1;
     }
     if (lane == 0) {
-        double vx = 0.0, vy = 0.0;
-        if (inliers >= c.min_inl) { vx = dtdx; vy = dtdy; }  // vFlow.cpp:934-942
-        fit_store(c, e, vx, vy);
+        const bool acc = inliers >= c.min_inl;  // vFlow.cpp:934-942
+        fit_plane(c, e, acc ? dtdx : 0.0, acc ? dtdy : 0.0, acc);
     }
 }
 
@@ -2285,6 +2317,7 @@ struct farms_handle {
     int4 *link = nullptr;
     int32_t *Q = nullptr;
     int4 *qe = nullptr;
+    double2 *plane = nullptr;
     // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
     const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
     const uint32_t *ph_t = nullptr;
@@ -2337,7 +2370,7 @@ void dfree(T *&p) {
 void free_workspace(farms_handle *h) {
     dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
     dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->link);
-    dfree(h->Q); dfree(h->qe); dfree(h->wkey); dfree(h->wkey_sorted);
+    dfree(h->Q); dfree(h->qe); dfree(h->plane); dfree(h->wkey); dfree(h->wkey_sorted);
     dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
     for (auto &d : h->o_d) dfree(d);
     dfree(h->cub_tmp);
@@ -2360,7 +2393,7 @@ int ensure_capacity(farms_handle *h, int64_t n) {
     if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
         (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
         (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->link, cap)) ||
-        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->qe, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
+        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->qe, cap)) || (rc = dalloc(&h->plane, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
         (rc = dalloc(&h->valid, cap)) ||
         (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
         (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
@@ -2485,7 +2518,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.link = h->link;
-    c.Q = h->Q; c.qe = h->qe;
+    c.Q = h->Q; c.qe = h->qe; c.plane = h->plane;
     c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
     c.pcur = h->pcur; c.pend = h->pend;
@@ -2623,11 +2656,12 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     };
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     int fit_enqueued = 0, fit_waited = -1;
-    if (phase == 1) {  // the whole fit sweep, then back to the caller
+    if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
         while (fit_enqueued < n_fit_chunks) {
             int rc = enqueue_fit(fit_enqueued++);
             if (rc) return rc;
         }
+        hipLaunchKernelGGL(k_flow, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, 0, n);
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipGetLastError());
         farms_stats st{};
@@ -2651,6 +2685,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
             const int fl = std::min(f, n_fit_chunks - 1);
             if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
+        }
+        if (phase != 2) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
+            const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
+            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
         for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
             hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, FARMS_CHAIN_WPB)), dim3(64 * FARMS_CHAIN_WPB), 0, sc, c, a,

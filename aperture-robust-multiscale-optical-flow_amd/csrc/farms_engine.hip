@@ -30,13 +30,18 @@
 // rounded atan2 / sin / cos (farms_libm.h); see DESIGN.md §3.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <climits>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -1602,15 +1607,17 @@ __global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_cha
             const bool touched = nxt[i] < ce;
             const int k1 = k[i];
             const int e1 = touched ? nxt[i] : INT_MAX;
-            if ((bal[i] >> lane) & 1) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
-                int run_hi = k1;
-                if (touched) {  // the run's last in-chunk position (a longer run is rare)
-                    int nn = pnx[i];
-                    while (nn < ce) {
-                        ++run_hi;
-                        nn = run_hi + 1 <= kend[i] ? c.P[run_hi + 1] : INT_MAX;
-                    }
+            // one walk over the cell's in-chunk run (a longer run is rare): its last
+            // position and event, and the run entry after the chunk
+            int run_hi = k1, last = e1, nn = pnx[i];
+            if (touched) {
+                while (nn < ce) {
+                    ++run_hi;
+                    last = nn;
+                    nn = run_hi + 1 <= kend[i] ? c.P[run_hi + 1] : INT_MAX;
                 }
+            }
+            if ((bal[i] >> lane) & 1) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
                 CandHdr hd;
                 CandVal v;
                 hd.lin = (uint32_t)q | (snap[i].L > 0 ? kCandSnapOk : 0u);
@@ -1633,14 +1640,8 @@ __global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_cha
                 c.val_ring[kb] = v;
             }
             if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
-                int kk = k1 + 1, last = e1, nn = pnx[i];
-                while (nn < ce) {
-                    last = nn;
-                    ++kk;
-                    nn = kk <= kend[i] ? c.P[kk] : INT_MAX;
-                }
                 snap[i] = last != e1 ? chain_load(&c.evf[last]) : pf[i];
-                k[i] = kk;
+                k[i] = run_hi + 1;
                 nxt[i] = nn;
                 dirty |= 1u << i;
                 prefetch(i);
@@ -2496,6 +2497,33 @@ int ensure_sync_events(farms_handle *h, size_t count) {
     return FARMS_OK;
 }
 
+// FARMS_GRAPH experiment aid: a SIGSEGV inside the graph runtime prints the
+// host call stack (on an alternate signal stack: the fault may be a stack
+// overflow) before the process dies.
+static void graph_segv_handler(int sig) {
+    void *fr[48];
+    const int k = backtrace(fr, 48);
+    static const char msg[] = "[farms graph] SIGSEGV, host stack:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, k, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static void graph_segv_trace() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    static std::vector<char> alt(1 << 16);
+    stack_t ss{};
+    ss.ss_sp = alt.data();
+    ss.ss_size = alt.size();
+    sigaltstack(&ss, nullptr);
+    struct sigaction sa{};
+    sa.sa_handler = graph_segv_handler;
+    sa.sa_flags = SA_ONSTACK;
+    sigaction(SIGSEGV, &sa, nullptr);
+}
+
 // The whole per-event loop for n device-resident events.  on_super (may be
 // null) is called as soon as the work of pooling super-chunk S (events [p0,
 // p1)) is enqueued, with the event that marks its records final on the device:
@@ -2536,7 +2564,14 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.counters = h->counters;
     c.dbg_tc = h->counting ? h->dbg_tc : nullptr;
 
-    const bool prof = h->profiling;
+    // FARMS_GRAPH=1 (experiment): the two sweeps of a plain call are
+    // captured into a hipGraph, instantiated and launched once (no timing events).
+    // Not under HIP runtimes before 7.2 (PyTorch 2.10 bundles 7.0): their stream
+    // capture recurses without bound on this launch pattern.
+    static const int hip_rt = [] { int v = 0; return hipRuntimeGetVersion(&v) == hipSuccess ? v : 0; }();
+    const char *gm = getenv("FARMS_GRAPH");
+    const bool graph = gm && gm[0] == '1' && phase == 0 && !on_super && hip_rt >= 70200000;
+    const bool prof = h->profiling && !graph;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
     const int B = h->pool_batch;
     const int n_super = ceil_div(n_pool_chunks, B);
@@ -2654,6 +2689,14 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         return FARMS_OK;
     };
+    if (graph) graph_segv_trace();
+    if (graph && !serial) {  // the chain and pooling streams join the capture by a fork event on F
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        HIPCHK(hipEventRecord(ev_prep, s));
+        HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
+    } else if (graph) {
+        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    }
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     int fit_enqueued = 0, fit_waited = -1;
     if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
@@ -2722,6 +2765,26 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     if (n_super > 0) {
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
+    }
+    if (graph) {
+        std::fprintf(stderr, "[farms graph] enqueued; ending the capture\n");
+        const auto g0 = std::chrono::steady_clock::now();
+        hipGraph_t gr = nullptr;
+        HIPCHK(hipStreamEndCapture(s, &gr));
+        const auto g1 = std::chrono::steady_clock::now();
+        hipGraphExec_t ge = nullptr;
+        HIPCHK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+        const auto g2 = std::chrono::steady_clock::now();
+        HIPCHK(hipGraphLaunch(ge, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const auto g3 = std::chrono::steady_clock::now();
+        size_t nodes = 0;
+        HIPCHK(hipGraphGetNodes(gr, nullptr, &nodes));
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "[farms graph] nodes %zu end_capture %.3f ms instantiate %.3f ms launch+run %.3f ms\n",
+                     nodes, ms(g0, g1), ms(g1, g2), ms(g2, g3));
+        HIPCHK(hipGraphExecDestroy(ge));
+        HIPCHK(hipGraphDestroy(gr));
     }
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (h->counting) {

@@ -167,7 +167,7 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
          "kernel": "k_pool", "launches_per_step": pool_launches, "avg_launch_us": round(avg_us, 2),
          "dense_equiv_bytes_per_launch": round(dense_per_launch),
          "dense_equiv_GBps": round(dense_per_launch / (avg_us * 1e-6) / 1e9, 1) if avg_us > 0 else None}
-    if sq:
+    if sq and avg_us > 0:
         waves = max(sq["SQ_WAVES"], 1.0)
         wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
         # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; a wave64

@@ -2109,8 +2109,11 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #ifndef FARMS_POOL_WAVES
 #define FARMS_POOL_WAVES 1  // minimum waves per SIMD requested of the register allocator
 #endif
-#ifndef FARMS_POOL_VGPR_FLOOR
-#define FARMS_POOL_VGPR_FLOOR "v79"  // k_pool occupancy cap (see k_pool)
+#ifndef FARMS_POOL_FLOOR_7
+#define FARMS_POOL_FLOOR_7 "v71"  // k_pool occupancy cap of 7 waves per SIMD (see k_pool)
+#endif
+#ifndef FARMS_POOL_FLOOR_6
+#define FARMS_POOL_FLOOR_6 "v79"  // k_pool occupancy cap of 6 waves per SIMD
 #endif
 #ifndef FARMS_POOL_EPW
 #define FARMS_POOL_EPW 1  // work-order positions per pooling wave
@@ -2118,7 +2121,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
 #ifndef FARMS_POOL_WPB
 #define FARMS_POOL_WPB 1  // waves (events) per k_pool workgroup: one, so that a finished event frees its slot at once
 #endif
-template <int K>
+template <int K, bool W7>
 __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
     // LDS per wave, sized for maxWindow M at launch: segment-start bitmap over
     // the flattened window, <= 2 row segments per window row, the values and
@@ -2126,12 +2129,16 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // Occupancy cap: the kernel allocates at least 80 VGPRs, i.e. at most 6
-    // pooling waves per SIMD (70 would allow 7).  The fit sweep's waves need
-    // the room: each of its 1,500 launches per C3 step waits for its slowest
-    // wave, so crowding them stretches the whole pipeline (measured at C3:
-    // 6 waves/SIMD 109.9 ms per step, 7: 122.0, 5: 113.9).
-    asm volatile("" ::: FARMS_POOL_VGPR_FLOOR);
+    // Occupancy cap: the kernel allocates at least 72 VGPRs (W7: at most 7
+    // pooling waves per SIMD) or 80 (6 waves).  The fit sweep's waves need the
+    // room: each of its launches waits for its slowest wave, so crowding them
+    // stretches the whole pipeline.  The optimum moves with the fit's weight: 6
+    // waves/SIMD won while the fit carried the libm chain (C3: 6 waves 109.9 ms
+    // per step, 7: 122.0, 5: 113.9); with k_flow split out, C3 runs 7 waves in
+    // 86.7-87.2 ms, 6: 89.9-90.3, 8 (64 VGPRs, 5 spills): 101.9, 5: 96.4; the
+    // heavier fs-7 fit (C4/C5) still wants 6 (pool_for).
+    if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
+    else asm volatile("" ::: FARMS_POOL_FLOOR_6);
     uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolValWords);
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
@@ -2429,25 +2436,34 @@ int reset_surfaces(farms_handle *h) {
     return FARMS_OK;
 }
 
-template <int K>
+template <int K, bool W7>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
     const int waves = c1 - c0;
     const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
-    hipLaunchKernelGGL(k_pool<K>, dim3(ceil_div(waves, FARMS_POOL_WPB * FARMS_POOL_EPW)), dim3(64 * FARMS_POOL_WPB), lds, s,
+    hipLaunchKernelGGL((k_pool<K, W7>), dim3(ceil_div(waves, FARMS_POOL_WPB * FARMS_POOL_EPW)), dim3(64 * FARMS_POOL_WPB), lds, s,
                        c, c0, c1);
 }
 
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
-pool_launcher pool_for(int K) {
+template <bool W7>
+pool_launcher pool_for_cap(int K) {
     switch (K) {
-    case 1: return launch_pool<1>;   case 2: return launch_pool<2>;   case 3: return launch_pool<3>;
-    case 4: return launch_pool<4>;   case 5: return launch_pool<5>;   case 6: return launch_pool<6>;
-    case 7: return launch_pool<7>;   case 8: return launch_pool<8>;   case 9: return launch_pool<9>;
-    case 10: return launch_pool<10>; case 11: return launch_pool<11>; case 12: return launch_pool<12>;
-    case 13: return launch_pool<13>; case 14: return launch_pool<14>; case 15: return launch_pool<15>;
-    case 16: return launch_pool<16>;
+    case 1: return launch_pool<1, W7>;   case 2: return launch_pool<2, W7>;   case 3: return launch_pool<3, W7>;
+    case 4: return launch_pool<4, W7>;   case 5: return launch_pool<5, W7>;   case 6: return launch_pool<6, W7>;
+    case 7: return launch_pool<7, W7>;   case 8: return launch_pool<8, W7>;   case 9: return launch_pool<9, W7>;
+    case 10: return launch_pool<10, W7>; case 11: return launch_pool<11, W7>; case 12: return launch_pool<12, W7>;
+    case 13: return launch_pool<13, W7>; case 14: return launch_pool<14, W7>; case 15: return launch_pool<15, W7>;
+    case 16: return launch_pool<16, W7>;
     default: return nullptr;
     }
+}
+// k_pool's occupancy cap by the fit's weight (see k_pool): 7 waves per SIMD
+// beside the fs <= 5 fits, 6 beside the heavier fs-7 and wave fits;
+// FARMS_POOL_CAP=6|7 overrides (tuning aid).
+pool_launcher pool_for(int K, int fr) {
+    bool w7 = fr <= 2;
+    if (const char *v = getenv("FARMS_POOL_CAP")) w7 = v[0] == '7';
+    return w7 ? pool_for_cap<true>(K) : pool_for_cap<false>(K);
 }
 
 // Fit of chunk [c0, c1); pr.blocks > 0: with the next chunk's prep riding on
@@ -2635,7 +2651,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     const char *ser = getenv("FARMS_SERIALIZE");
     const bool serial = ser && ser[0] == '1';
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
-    pool_launcher pl = pool_for(h->K);
+    pool_launcher pl = pool_for(h->K, h->fr);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
     const bool fit_quad = !(fq && fq[0] == '0');
@@ -2925,6 +2941,25 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, pr[1]) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, pr[2]) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
+    // FARMS_POOL_CU_SKIP = k (0..4): k CUs per XCD left out of the pooling
+    // stream's CU mask, so the fit chain always finds free slots there.  Bits
+    // 32j + 8t + j (t < k): k per 32-bit word and k per residue mod 8, whichever
+    // way the mask bits map to XCDs.
+    if (const char *v = getenv("FARMS_POOL_CU_SKIP")) {
+        const int k = std::max(0, std::min(atoi(v), 4));
+        int dev = 0;
+        hipDeviceProp_t dp{};
+        if (k > 0 && hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&dp, dev) == hipSuccess &&
+            dp.multiProcessorCount % 32 == 0) {
+            const int ncu = dp.multiProcessorCount;
+            std::vector<uint32_t> m((size_t)ncu / 32, 0xffffffffu);
+            for (int j = 0; j < ncu / 32; ++j)
+                for (int t = 0; t < k; ++t) m[j] &= ~(1u << (8 * t + (j & 7)));
+            if (hipStreamDestroy(h->s_pool) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&h->s_pool, (uint32_t)m.size(), m.data()) != hipSuccess)
+                return bail(fail(FARMS_EHIP, "hipExtStreamCreateWithCUMask"));
+        }
+    }
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||

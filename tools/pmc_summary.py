@@ -9,8 +9,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 for r in rows:
-    m = re.search(r"(k_\w+(<\d+>)?)", r["Kernel_Name"])
-    k = m.group(1) if m else r["Kernel_Name"][:40]
+    m = re.search(r"(k_\w+)(?:<(\d+)[^>]*>)?", r["Kernel_Name"])  # k_pool<11, true> -> k_pool<11>
+    k = (m.group(1) + (f"<{m.group(2)}>" if m.group(2) else "")) if m else r["Kernel_Name"][:40]
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     disp[k].add(r["Dispatch_Id"])
 for k, v in agg.items():

@@ -21,8 +21,8 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"(k_\w+(<\d+>)?)", r["Kernel_Name"])
-        k = m.group(1) if m else r["Kernel_Name"][:40]
+        m = re.search(r"(k_\w+)(?:<(\d+)[^>]*>)?", r["Kernel_Name"])  # k_pool<11, true> -> k_pool<11>
+        k = (m.group(1) + (f"<{m.group(2)}>" if m.group(2) else "")) if m else r["Kernel_Name"][:40]
         tot[k] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     return tot, {k: len(v) for k, v in disp.items()}

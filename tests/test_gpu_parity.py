@@ -111,6 +111,19 @@ def test_chunking_is_bitwise_invariant():
         assert bitwise_equal(outs[0], o)
 
 
+def test_pool_occupancy_cap_is_bitwise_invariant(monkeypatch):
+    """k_pool is built twice (7- and 6-wave VGPR floors, pool_for picks by
+    filter size): both builds give the same bits."""
+    ev = farms.synth_config(3, 120_000)
+    x, y, t, p = ev.relative()
+    outs = []
+    for cap in ("7", "6"):
+        monkeypatch.setenv("FARMS_POOL_CAP", cap)
+        with farms.FlowManager(720, 1280, 5, 5) as fm:
+            outs.append(fm.process(x, y, t, p))
+    assert bitwise_equal(outs[0], outs[1])
+
+
 def test_streaming_split_equals_one_call():
     ev = farms.synth_config(2, 150_000)
     x, y, t, p = ev.relative()

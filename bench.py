@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--events", type=int, default=0, help="override the stream length")
     ap.add_argument("--fit-chunk", type=int, default=0)
     ap.add_argument("--pool-chunk", type=int, default=0)
+    ap.add_argument("--pool-batch", type=int, default=0, help="pooling chunks per k_pool launch (0 = engine default)")
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
     ap.add_argument("--parity-sample", type=int, default=300_000,
                     help="N > 1: rank 0 checks its records of the stream's first K events against the oracle")
@@ -345,8 +346,8 @@ def main():
            for c in farms.COLUMNS[4:]}
     lists = sh.get("lists")
     fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, region=sh["region"], owned=sh["owned"],
-                           import_halo=lists is not None)
+                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, pool_batch=args.pool_batch,
+                           region=sh["region"], owned=sh["owned"], import_halo=lists is not None)
     if lists is not None:  # flow-halo exchange buffers, per peer
         xdev = dev if backend == "nccl" else torch.device("cpu")
         send_idx = {q: torch.from_numpy(a).to(dev) for q, (a, _) in lists.items()}

@@ -436,6 +436,11 @@ __global__ void k_fit_prep(Ctx c, SaeCell *cells, int p0, int c0, int c1, uint32
 // the fit's grid): it writes the other SAE buffer, which the fit of chunk f
 // does not read, and the fit of chunk f-1 (the buffer's last reader) finished
 // with the previous launch.
+#ifndef FARMS_FIT_PREP_FIRST
+// 1: the riding prep takes a fit launch's first blocks instead of its last
+// (A/B at C3: 557-559 Mevents/s against 574: the fit sweep stretches 79 -> 83 ms)
+#define FARMS_FIT_PREP_FIRST 0
+#endif
 struct FitPrep {
     SaeCell *cells;
     int p0, c0, c1;
@@ -1280,11 +1285,22 @@ template <int FR, bool UT>
 __global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
     fit_prio();
     const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
+#if FARMS_FIT_PREP_FIRST
+    // the next chunk's prep in the first blocks (a multiple of 8: the fit's
+    // blocks keep their XCDs)
+    if ((int)blockIdx.x < pr.blocks) {
+        fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq, (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x);
+        return;
+    }
+    const int bid = (int)blockIdx.x - pr.blocks;
+#else
     if ((int)blockIdx.x >= G) {
         fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
                         ((int)blockIdx.x - G) * (int)blockDim.x + (int)threadIdx.x);
         return;
     }
+    const int bid = (int)blockIdx.x;
+#endif
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
@@ -1292,7 +1308,7 @@ __global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_qua
 #ifndef FARMS_FIT_XCD
 #define FARMS_FIT_XCD 1
 #endif
-    const int fb = FARMS_FIT_XCD ? xcd_block_grouped((int)blockIdx.x, G) : (int)blockIdx.x;
+    const int fb = FARMS_FIT_XCD ? xcd_block_grouped(bid, G) : bid;
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -2669,6 +2685,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     auto prep_of = [&](int f) {  // the prep of chunk f (into buffer f % 2); blocks for 64-thread blocks
         FitPrep pr{cells_of(f), fit_start(std::max(f - 2, 0)), fit_start(f), fit_chunk_end(f), seq_base + f + 1, 0};
         pr.blocks = ceil_div(std::max(pr.c1 - pr.c0, pr.c0 - pr.p0), 64);
+        if (FARMS_FIT_PREP_FIRST) pr.blocks = (pr.blocks + 7) & ~7;  // whole rounds of the 8 XCDs
         return pr;
     };
     auto launch_prep = [&](const FitPrep &pr) {

@@ -140,11 +140,27 @@ struct __attribute__((aligned(16))) BmWord {
     uint32_t wo;
     uint32_t pad;
 };
+#ifndef FARMS_CAND_SPLIT
+#define FARMS_CAND_SPLIT 0  // 1: payload as two 32-B aligned halves, each written only when read (A/B: 574 vs 575-578 Mevents/s, off)
+#endif
+#if FARMS_CAND_SPLIT
+// Snapshot half and in-chunk half, each one 32-B sector: a contributor's value
+// load touches one sector, and k_chain skips the halves k_pool never reads
+// (the snapshot of a cell without a valid one, the in-chunk half of an
+// untouched cell).
+struct __attribute__((aligned(32))) CandVal {
+    double L_snap, Lc_snap, Ls_snap;
+    uint64_t pad;
+    double L1, Lc1, Ls1;
+    int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
+};
+#else
 struct CandVal {
     double L_snap, Lc_snap, Ls_snap;
     double L1, Lc1, Ls1;
     int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
 };
+#endif
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 // LDS packing of k_pool's row segments (32 bits each):
@@ -1653,7 +1669,16 @@ __global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_cha
                 }
                 const int64_t kb = (int64_t)b * c.cstride + woff[i] + (uint32_t)__popcll(bal[i] & lt);
                 c.hdr_ring[kb] = hd;
+#if FARMS_CAND_SPLIT
+                CandVal *vo = c.val_ring + kb;
+                if (snap[i].L > 0) { vo->L_snap = v.L_snap; vo->Lc_snap = v.Lc_snap; vo->Ls_snap = v.Ls_snap; }
+                if (touched) {
+                    vo->L1 = v.L1; vo->Lc1 = v.Lc1; vo->Ls1 = v.Ls1;
+                    vo->run_lo = v.run_lo; vo->run_hi = v.run_hi;
+                }
+#else
                 c.val_ring[kb] = v;
+#endif
             }
             if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
                 snap[i] = last != e1 ? chain_load(&c.evf[last]) : pf[i];

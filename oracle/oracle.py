@@ -13,7 +13,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libfarms_oracle.so")
+# FARMS_ORACLE_LIB: another build of the same oracle (the -O0 CPU-baseline leg,
+# tools/cpu_baseline_configs.py); the tests and the bench never set it
+LIB = os.environ.get("FARMS_ORACLE_LIB") or os.path.join(HERE, "build", "libfarms_oracle.so")
 
 _lib = None
 

@@ -1765,6 +1765,9 @@ __device__ __forceinline__ double wave_max(double v) {
 #ifndef FARMS_POOL_FOLD_ASM
 #define FARMS_POOL_FOLD_ASM 1  // 0: the fold as masked fmas in C (A/B aid)
 #endif
+#ifndef FARMS_POOL_FOLD_PIPE
+#define FARMS_POOL_FOLD_PIPE 0  // 1: the asm fold's LDS reads one trip ahead; 2: fold8 as two fold4 halves
+#endif
 #if FARMS_POOL_FOLD_ASM && FARMS_POOL_UNROLL != 8
 #error "the asm fold takes 8 entries per trip"
 #endif
@@ -1811,6 +1814,28 @@ __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_
           [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [sv] "=&s"(sv)
         : [kk] "v"(kk), [kw0] "v"(kw0), [kw1] "v"(kw1), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]),
           [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7]));
+}
+// Half of fold8 (entries b0..b3 of one k0 word): the second half's LDS reads
+// can still be in flight while the first half's adds run.
+__device__ __forceinline__ void fold4(double &acc, int kk, uint32_t kw, double v0, double v1, double v2, double v3) {
+    uint64_t m0, m1, m2, m3, sv;
+    asm volatile(
+        "v_cmp_ge_i32_sdwa %[m0], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_0\n"
+        "v_cmp_ge_i32_sdwa %[m1], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_1\n"
+        "v_cmp_ge_i32_sdwa %[m2], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_2\n"
+        "v_cmp_ge_i32_sdwa %[m3], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_3\n"
+        "s_mov_b64 %[sv], exec\n"
+        "s_mov_b64 exec, %[m0]\n"
+        "v_add_f64 %[acc], %[acc], %[v0]\n"
+        "s_mov_b64 exec, %[m1]\n"
+        "v_add_f64 %[acc], %[acc], %[v1]\n"
+        "s_mov_b64 exec, %[m2]\n"
+        "v_add_f64 %[acc], %[acc], %[v2]\n"
+        "s_mov_b64 exec, %[m3]\n"
+        "v_add_f64 %[acc], %[acc], %[v3]\n"
+        "s_mov_b64 exec, %[sv]\n"
+        : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [sv] "=&s"(sv)
+        : [kk] "v"(kk), [kw] "v"(kw), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3));
 }
 // Row setup of a pooling window: the flattened candidate slices of rows
 // [i_lo, i_lo + nrows) (nrows <= 128), cells j in [j_lo, j_hi] of each row
@@ -2071,6 +2096,28 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+#if FARMS_POOL_FOLD_ASM && FARMS_POOL_FOLD_PIPE == 1
+            // software-pipelined: the next trip's k0 words and values are read
+            // from LDS while this trip's dependent adds run (a trip past cnt
+            // re-reads the current one: wave-uniform clamp, slots stay in range)
+            uint32_t kwa = k4p[0], kwb = k4p[1];
+            double vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * u + grp];
+#pragma unroll 1
+            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += 8) {
+                const int rn = r + 8 < cnt ? r + 8 : r;
+                const uint32_t na = k4p[rn >> 2], nb = k4p[(rn >> 2) + 1];
+                double nv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) nv[u] = s_val[4 * (rn + u) + grp];
+                fold8(acc, kk, kwa, kwb, vv);
+                kwa = na; kwb = nb;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vv[u] = nv[u];
+            }
+            if (false)
+#endif
 #pragma unroll 1
             for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // slots past cnt: k0 = K
                 uint32_t kw[FARMS_POOL_UNROLL / 4];
@@ -2080,7 +2127,12 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 double vv[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
+#if FARMS_POOL_FOLD_PIPE == 2
+                fold4(acc, kk, kw[0], vv[0], vv[1], vv[2], vv[3]);
+                fold4(acc, kk, kw[1], vv[4], vv[5], vv[6], vv[7]);
+#else
                 fold8(acc, kk, kw[0], kw[1], vv);
+#endif
 #else
                 // members as fma(v, 1, acc) = acc + v, non-members as fma(v, 0,
                 // acc) = acc + (+-0) = acc: acc starts at +0 and a round-to-

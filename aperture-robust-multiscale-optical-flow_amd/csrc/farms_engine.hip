@@ -30,9 +30,6 @@
 // rounded atan2 / sin / cos (farms_libm.h); see DESIGN.md §3.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
-#include <execinfo.h>
-#include <signal.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -54,19 +51,9 @@
 #include "../../include/farms_hip.h"
 #include "farms_libm.h"
 
-// FARMS_OCML_LIBM=1: ROCm's faithful (not correctly rounded) atan2/sin/cos
-// instead of farms_libm.h -- A/B aid only, breaks bitwise parity
-#if defined(FARMS_OCML_LIBM) && FARMS_OCML_LIBM
-#define F_ATAN2 ::atan2
-#define F_COS ::cos
-#define F_SIN ::sin
-#define F_SINCOS ::sincos
-#else
+// correctly rounded atan2 / sincos (farms_libm.h)
 #define F_ATAN2 farms_libm::cr_atan2
-#define F_COS farms_libm::cr_cos
-#define F_SIN farms_libm::cr_sin
 #define F_SINCOS farms_libm::cr_sincos
-#endif
 
 namespace {
 
@@ -140,27 +127,11 @@ struct __attribute__((aligned(16))) BmWord {
     uint32_t wo;
     uint32_t pad;
 };
-#ifndef FARMS_CAND_SPLIT
-#define FARMS_CAND_SPLIT 0  // 1: payload as two 32-B aligned halves, each written only when read (A/B: 574 vs 575-578 Mevents/s, off)
-#endif
-#if FARMS_CAND_SPLIT
-// Snapshot half and in-chunk half, each one 32-B sector: a contributor's value
-// load touches one sector, and k_chain skips the halves k_pool never reads
-// (the snapshot of a cell without a valid one, the in-chunk half of an
-// untouched cell).
-struct __attribute__((aligned(32))) CandVal {
-    double L_snap, Lc_snap, Ls_snap;
-    uint64_t pad;
-    double L1, Lc1, Ls1;
-    int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
-};
-#else
 struct CandVal {
     double L_snap, Lc_snap, Ls_snap;
     double L1, Lc1, Ls1;
     int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
 };
-#endif
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 // LDS packing of k_pool's row segments (32 bits each):
@@ -278,21 +249,14 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
 // Grouped variant: runs of 8 consecutive logical blocks stay on one XCD and
 // the runs go round-robin over the XCDs (locality without uneven shares).
 // Bijective on [0, G) when G is a multiple of 64; other grids keep blockIdx.
-#ifndef FARMS_FIT_RUN
-#define FARMS_FIT_RUN 8  // consecutive blocks per XCD run
-#endif
+constexpr int kFitRun = 8;  // consecutive fit blocks per XCD run
 __device__ __forceinline__ int xcd_block_grouped(int b, int G) {
-    constexpr int R = FARMS_FIT_RUN;
+    constexpr int R = kFitRun;
     if (G % (8 * R)) return b;
     const int x = b & 7, i = b >> 3;  // XCD label, index within the XCD
     return (i / R) * (8 * R) + x * R + (i % R);
 }
-#ifndef FARMS_XCD
-#define FARMS_XCD 1  // 0: plain blockIdx order (A/B aid)
-#endif
-__device__ __forceinline__ int work_block() {
-    return FARMS_XCD ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-}
+__device__ __forceinline__ int work_block() { return xcd_block((int)blockIdx.x, (int)gridDim.x); }
 
 // ---------------------------------------------------------------------------
 // prep
@@ -377,20 +341,6 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
 // it (chunks f-2 and f-1: the buffer last served chunk f-2), set the snapshot
 // of the pixels they touched that chunk f does not touch to their last event.
 // The two parts write disjoint cells.
-// Wave priority of the fit sweep's kernels: each fit launch waits for its
-// predecessor's slowest wave, and those waves share their SIMDs with the
-// pooling waves of the stream beside it; raising their issue priority keeps
-// the fit chain from stretching (FARMS_FIT_PRIO 0 = none).
-#ifndef FARMS_FIT_PRIO
-#define FARMS_FIT_PRIO 0
-#endif
-__device__ __forceinline__ void fit_prio() {
-    if (FARMS_FIT_PRIO) __builtin_amdgcn_s_setprio(FARMS_FIT_PRIO);
-}
-#ifndef FARMS_CHAIN_PRIO
-#define FARMS_CHAIN_PRIO 0
-#endif
-
 __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq,
                                                 int i) {
     const int ep = p0 + i;
@@ -444,19 +394,14 @@ __global__ void k_pool_desc(Ctx c, int p0, int p1) {
 // The prep of one fit chunk as its own launch (the first chunk of a call, the
 // final commits, the fit paths without a merged prep).
 __global__ void k_fit_prep(Ctx c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq) {
-    fit_prio();
     fit_prep_thread(c, cells, p0, c0, c1, seq, (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
 
 // The prep of fit chunk f+1 riding on the launch of fit chunk f (blocks past
-// the fit's grid): it writes the other SAE buffer, which the fit of chunk f
-// does not read, and the fit of chunk f-1 (the buffer's last reader) finished
-// with the previous launch.
-#ifndef FARMS_FIT_PREP_FIRST
-// 1: the riding prep takes a fit launch's first blocks instead of its last
-// (A/B at C3: 557-559 Mevents/s against 574: the fit sweep stretches 79 -> 83 ms)
-#define FARMS_FIT_PREP_FIRST 0
-#endif
+// the fit's grid; in the first blocks it measured slower, the fit sweep
+// stretching 79 -> 83 ms at C3): it writes the other SAE buffer, which the fit
+// of chunk f does not read, and the fit of chunk f-1 (the buffer's last reader)
+// finished with the previous launch.
 struct FitPrep {
     SaeCell *cells;
     int p0, c0, c1;
@@ -853,7 +798,15 @@ __global__ void k_flow(Ctx c, int e0, int e1) {
     if (e >= e1) return;
     if (!c.fit_all) {
         const int ex = c.x[e];
-        if (ex < c.fit_lo || ex >= c.fit_hi) return;
+        if (ex < c.fit_lo || ex >= c.fit_hi) {
+            // a halo event: invalid until farms_import_flows supplies its
+            // owner's flow (a flow never imported is not pooled, never stale)
+            FlowCell f;
+            f.L = 0.0; f.Lc = 0.0; f.Ls = 0.0; f.t = c.t[e]; f.pad = 0;
+            c.evf[e] = f;
+            c.valid[e] = 0;
+            return;
+        }
     }
     double vx = 0.0, vy = 0.0;
     if (c.valid[e]) {
@@ -939,10 +892,9 @@ __device__ __forceinline__ uint64_t quad_or_u64(uint64_t v) {
     return v | ((uint64_t)(uint32_t)xch32<1>(hi) << 32) | (uint32_t)xch32<1>(lo);
 }
 
-#ifndef FARMS_FIT_WPB
-#define FARMS_FIT_WPB 1  // waves per k_fit_quad workgroup (16 events each)
-#endif
-constexpr int kFitQS = 16 * FARMS_FIT_WPB;  // quads per fit workgroup: stride of the LDS stamp tiles
+// one-wave k_fit_quad workgroups (16 events each): a finished wave frees its
+// slot at once (4-wave groups held it for their slowest event)
+constexpr int kFitQS = 16;  // quads per fit workgroup: stride of the LDS stamp tiles
 
 template <int FR>
 __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq, int j, uint32_t *lt, double &vx_out,
@@ -1294,37 +1246,20 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t s
 }
 
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
-#ifndef FARMS_FIT_WAVES
-#define FARMS_FIT_WAVES 1  // minimum waves per SIMD requested of the register allocator
-#endif
 template <int FR, bool UT>
-__global__ __launch_bounds__(64 * FARMS_FIT_WPB, FARMS_FIT_WAVES) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
-    fit_prio();
+__global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
     const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
-#if FARMS_FIT_PREP_FIRST
-    // the next chunk's prep in the first blocks (a multiple of 8: the fit's
-    // blocks keep their XCDs)
-    if ((int)blockIdx.x < pr.blocks) {
-        fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq, (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x);
-        return;
-    }
-    const int bid = (int)blockIdx.x - pr.blocks;
-#else
     if ((int)blockIdx.x >= G) {
         fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
                         ((int)blockIdx.x - G) * (int)blockDim.x + (int)threadIdx.x);
         return;
     }
     const int bid = (int)blockIdx.x;
-#endif
     constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
     // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
-#ifndef FARMS_FIT_XCD
-#define FARMS_FIT_XCD 1
-#endif
-    const int fb = FARMS_FIT_XCD ? xcd_block_grouped(bid, G) : bid;
+    const int fb = xcd_block_grouped(bid, G);
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -1554,16 +1489,11 @@ __device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
     const FlowCell f = *p;
     return ChainFlow{f.L, f.Lc, f.Ls, f.t};
 }
-#ifndef FARMS_CHAIN_WPB
-#define FARMS_CHAIN_WPB 1  // waves per k_chain workgroup (the waves are independent)
-#endif
-#ifndef FARMS_CHAIN_WAVES
-#define FARMS_CHAIN_WAVES 4  // k_chain waves per SIMD the register allocation must allow
-#endif
-__global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0, int ch1) {
-    if (FARMS_CHAIN_PRIO) __builtin_amdgcn_s_setprio(FARMS_CHAIN_PRIO);
+// One-wave workgroups (a 4-wave one needs 4 x 128 VGPRs free at once on one
+// CU, which the pooling waves rarely leave), at most 128 VGPRs (4 waves per SIMD).
+__global__ __launch_bounds__(64, 4) void k_chain(Ctx c, int ch0, int ch1) {
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * FARMS_CHAIN_WPB + (threadIdx.x >> 6);
+    const int64_t g = (int64_t)blockIdx.x;
     if (g >= c.nblk) return;
     const int n = c.n, C2 = c.C2;
     const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
@@ -1669,16 +1599,7 @@ __global__ __launch_bounds__(64 * FARMS_CHAIN_WPB, FARMS_CHAIN_WAVES) void k_cha
                 }
                 const int64_t kb = (int64_t)b * c.cstride + woff[i] + (uint32_t)__popcll(bal[i] & lt);
                 c.hdr_ring[kb] = hd;
-#if FARMS_CAND_SPLIT
-                CandVal *vo = c.val_ring + kb;
-                if (snap[i].L > 0) { vo->L_snap = v.L_snap; vo->Lc_snap = v.Lc_snap; vo->Ls_snap = v.Ls_snap; }
-                if (touched) {
-                    vo->L1 = v.L1; vo->Lc1 = v.Lc1; vo->Ls1 = v.Ls1;
-                    vo->run_lo = v.run_lo; vo->run_hi = v.run_hi;
-                }
-#else
                 c.val_ring[kb] = v;
-#endif
             }
             if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
                 snap[i] = last != e1 ? chain_load(&c.evf[last]) : pf[i];
@@ -1756,21 +1677,6 @@ __device__ __forceinline__ double wave_max(double v) {
 //   fold them into the per-scale sums in the reference's order (pool_one).
 // The summation order depends only on the contributor list, so results are
 // bitwise independent of chunking and streaming splits.
-#ifndef FARMS_POOL_STOP
-#define FARMS_POOL_STOP 0  // ablation aid (variants only): 1 row setup only, 3 all but the folds
-#endif
-#ifndef FARMS_POOL_UNROLL
-#define FARMS_POOL_UNROLL 8  // fold entries per loop trip (4 or 8; 64 must be a multiple)
-#endif
-#ifndef FARMS_POOL_FOLD_ASM
-#define FARMS_POOL_FOLD_ASM 1  // 0: the fold as masked fmas in C (A/B aid)
-#endif
-#ifndef FARMS_POOL_FOLD_PIPE
-#define FARMS_POOL_FOLD_PIPE 0  // 1: the asm fold's LDS reads one trip ahead; 2: fold8 as two fold4 halves
-#endif
-#if FARMS_POOL_FOLD_ASM && FARMS_POOL_UNROLL != 8
-#error "the asm fold takes 8 entries per trip"
-#endif
 // Fold of 8 staged entries into this lane's sum: entry u (smallest scale k0 =
 // byte u of kw0:kw1) is added iff kk >= k0, as an exec-masked v_add_f64: the
 // member test runs once per entry for all lanes (v_cmp into an SGPR mask, all
@@ -1780,7 +1686,10 @@ __device__ __forceinline__ double wave_max(double v) {
 // compare, a select and an fma).  exec is restored before the asm ends.  The
 // masks are subsets of exec (v_cmp writes 0 for inactive lanes), so exec is set
 // with s_mov_b64, which leaves SCC alone: the surrounding code may hold a
-// loop condition there (s_and_b64 would clobber it).
+// loop condition there (s_and_b64 would clobber it).  (The same sum as a
+// masked fma, fma(v, m, acc) with m in {0, 1}, is bitwise equal -- acc starts
+// at +0 and a round-to-nearest sum is -0 only when both addends are -- but
+// costs a compare, a select and an fma per entry.)
 __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_t kw1, const double (&v)[8]) {
     uint64_t m0, m1, m2, m3, m4, m5, m6, m7, sv;
     asm volatile(
@@ -1814,28 +1723,6 @@ __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_
           [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [sv] "=&s"(sv)
         : [kk] "v"(kk), [kw0] "v"(kw0), [kw1] "v"(kw1), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]),
           [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7]));
-}
-// Half of fold8 (entries b0..b3 of one k0 word): the second half's LDS reads
-// can still be in flight while the first half's adds run.
-__device__ __forceinline__ void fold4(double &acc, int kk, uint32_t kw, double v0, double v1, double v2, double v3) {
-    uint64_t m0, m1, m2, m3, sv;
-    asm volatile(
-        "v_cmp_ge_i32_sdwa %[m0], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_0\n"
-        "v_cmp_ge_i32_sdwa %[m1], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_1\n"
-        "v_cmp_ge_i32_sdwa %[m2], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_2\n"
-        "v_cmp_ge_i32_sdwa %[m3], %[kk], %[kw] src0_sel:DWORD src1_sel:BYTE_3\n"
-        "s_mov_b64 %[sv], exec\n"
-        "s_mov_b64 exec, %[m0]\n"
-        "v_add_f64 %[acc], %[acc], %[v0]\n"
-        "s_mov_b64 exec, %[m1]\n"
-        "v_add_f64 %[acc], %[acc], %[v1]\n"
-        "s_mov_b64 exec, %[m2]\n"
-        "v_add_f64 %[acc], %[acc], %[v2]\n"
-        "s_mov_b64 exec, %[m3]\n"
-        "v_add_f64 %[acc], %[acc], %[v3]\n"
-        "s_mov_b64 exec, %[sv]\n"
-        : [acc] "+v"(acc), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [sv] "=&s"(sv)
-        : [kk] "v"(kk), [kw] "v"(kw), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3));
 }
 // Row setup of a pooling window: the flattened candidate slices of rows
 // [i_lo, i_lo + nrows) (nrows <= 128), cells j in [j_lo, j_hi] of each row
@@ -1970,10 +1857,6 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     const uint32_t own_lin = c.serial ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
     const uint32_t own_tprev = c.serial ? (uint32_t)c.link[e].w : 0u;
     (void)ev0;
-#if FARMS_POOL_STOP == 1
-    if (lane == 0) c.scale[e] = total;  // ablation: row setup only
-    return;
-#endif
     // lane g*K + kk: quantity g of scale kk, g = 0..3 (L, L cos, L sin, and the
     // contributor count as a sum of 1.0: exact); lanes past 4K fold junk
     const int grp = lane / K < 3 ? lane / K : 3;
@@ -2096,56 +1979,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
-#if FARMS_POOL_FOLD_ASM && FARMS_POOL_FOLD_PIPE == 1
-            // software-pipelined: the next trip's k0 words and values are read
-            // from LDS while this trip's dependent adds run (a trip past cnt
-            // re-reads the current one: wave-uniform clamp, slots stay in range)
-            uint32_t kwa = k4p[0], kwb = k4p[1];
-            double vv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * u + grp];
 #pragma unroll 1
-            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += 8) {
-                const int rn = r + 8 < cnt ? r + 8 : r;
-                const uint32_t na = k4p[rn >> 2], nb = k4p[(rn >> 2) + 1];
-                double nv[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) nv[u] = s_val[4 * (rn + u) + grp];
-                fold8(acc, kk, kwa, kwb, vv);
-                kwa = na; kwb = nb;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) vv[u] = nv[u];
-            }
-            if (false)
-#endif
-#pragma unroll 1
-            for (int r = 0; r < (FARMS_POOL_STOP == 3 ? 0 : cnt); r += FARMS_POOL_UNROLL) {  // slots past cnt: k0 = K
-                uint32_t kw[FARMS_POOL_UNROLL / 4];
-#pragma unroll
-                for (int u = 0; u < FARMS_POOL_UNROLL / 4; ++u) kw[u] = k4p[(r >> 2) + u];
-#if FARMS_POOL_FOLD_ASM
+            for (int r = 0; r < cnt; r += 8) {  // slots past cnt: k0 = K (in no scale)
+                const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
                 double vv[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
-#if FARMS_POOL_FOLD_PIPE == 2
-                fold4(acc, kk, kw[0], vv[0], vv[1], vv[2], vv[3]);
-                fold4(acc, kk, kw[1], vv[4], vv[5], vv[6], vv[7]);
-#else
-                fold8(acc, kk, kw[0], kw[1], vv);
-#endif
-#else
-                // members as fma(v, 1, acc) = acc + v, non-members as fma(v, 0,
-                // acc) = acc + (+-0) = acc: acc starts at +0 and a round-to-
-                // nearest sum is -0 only when both addends are, so this is
-                // bitwise the conditional add (valid flows are finite)
-#pragma unroll
-                for (int u = 0; u < FARMS_POOL_UNROLL; ++u) {
-                    const int k0u = (int)((kw[u >> 2] >> (8 * (u & 3))) & 0xFFu);
-                    const double vu = s_val[4 * (r + u) + grp];
-                    const double m = kk >= k0u ? 1.0 : 0.0;
-                    acc = __builtin_fma(vu, m, acc);
-                }
-#endif
+                fold8(acc, kk, kw0, kw1, vv);
             }
             ncon_total += cnt;
         }
@@ -2196,32 +2036,20 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0);
 }
 
-// One wavefront per work-order position of [c0, c1) (events of a chunk in
-// tile order); invalid events and halo events (fitted here, pooled by their
-// owner) leave at once.
-#ifndef FARMS_POOL_WAVES
-#define FARMS_POOL_WAVES 1  // minimum waves per SIMD requested of the register allocator
-#endif
-#ifndef FARMS_POOL_FLOOR_7
+// One wavefront (= one workgroup, so that a finished event frees its slot at
+// once) per work-order position of [c0, c1) (events of a chunk in tile order);
+// invalid events and halo events (fitted here, pooled by their owner) leave at
+// once.
 #define FARMS_POOL_FLOOR_7 "v71"  // k_pool occupancy cap of 7 waves per SIMD (see k_pool)
-#endif
-#ifndef FARMS_POOL_FLOOR_6
 #define FARMS_POOL_FLOOR_6 "v79"  // k_pool occupancy cap of 6 waves per SIMD
-#endif
-#ifndef FARMS_POOL_EPW
-#define FARMS_POOL_EPW 1  // work-order positions per pooling wave
-#endif
-#ifndef FARMS_POOL_WPB
-#define FARMS_POOL_WPB 1  // waves (events) per k_pool workgroup: one, so that a finished event frees its slot at once
-#endif
 template <int K, bool W7>
-__global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(Ctx c, int c0, int c1) {
+__global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     // LDS per wave, sized for maxWindow M at launch: segment-start bitmap over
     // the flattened window, <= 2 row segments per window row, the values and
     // k0 of one step's 64 staged entries
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const int nbw = c.pool_bw, nrs = c.pool_rs;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     // Occupancy cap: the kernel allocates at least 72 VGPRs (W7: at most 7
     // pooling waves per SIMD) or 80 (6 waves).  The fit sweep's waves need the
     // room: each of its launches waits for its slowest wave, so crowding them
@@ -2232,23 +2060,19 @@ __global__ __launch_bounds__(64 * FARMS_POOL_WPB, FARMS_POOL_WAVES) void k_pool(
     // heavier fs-7 fit (C4/C5) still wants 6 (pool_for).
     if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
     else asm volatile("" ::: FARMS_POOL_FLOOR_6);
-    uint64_t *s_start = s_dyn + (size_t)wv * (nbw + nrs + kPoolValWords);
+    uint64_t *s_start = s_dyn;
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64 * FARMS_POOL_HALVES);
-    // FARMS_POOL_EPW consecutive work-order positions per wave (one chunk: C2
-    // is a multiple of it)
-    const int w0 = c0 + (work_block() * FARMS_POOL_WPB + wv) * FARMS_POOL_EPW;
-#pragma unroll 1
-    for (int w = w0; w < w0 + FARMS_POOL_EPW && w < c1; ++w) {
-        // the event and its fields in one 16-B load (k_pool_desc)
-        const int4 d = c.qe[w];
-        if (d.x < 0) continue;  // invalid flow, or a halo event (pooled by its owner)
-        const int e = d.x, ex = d.y, ey = d.z;
-        const uint32_t teu = (uint32_t)d.w;
-        const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-        pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
-    }
+    const int w = c0 + work_block();
+    if (w >= c1) return;
+    // the event and its fields in one 16-B load (k_pool_desc)
+    const int4 d = c.qe[w];
+    if (d.x < 0) return;  // invalid flow, or a halo event (pooled by its owner)
+    const int e = d.x, ex = d.y, ey = d.z;
+    const uint32_t teu = (uint32_t)d.w;
+    const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -2426,6 +2250,7 @@ struct farms_handle {
     farms_records ph_out{};
     int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
     uint32_t first_t = 0;
+    bool fresh = true;          // no event since create / reset (farms_serial_first's precondition)
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     int tile_bits = 0;
     int tile_shift = 3;       // work-order tile: 2^tile_shift square (FARMS_POOL_TILE)
@@ -2526,15 +2351,14 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     h->first_q = -1;
+    h->fresh = true;
     return FARMS_OK;
 }
 
 template <int K, bool W7>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
-    const int waves = c1 - c0;
-    const size_t lds = FARMS_POOL_WPB * sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
-    hipLaunchKernelGGL((k_pool<K, W7>), dim3(ceil_div(waves, FARMS_POOL_WPB * FARMS_POOL_EPW)), dim3(64 * FARMS_POOL_WPB), lds, s,
-                       c, c0, c1);
+    const size_t lds = sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
+    hipLaunchKernelGGL((k_pool<K, W7>), dim3(c1 - c0), dim3(64), lds, s, c, c0, c1);
 }
 
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
@@ -2564,7 +2388,7 @@ pool_launcher pool_for(int K, int fr) {
 bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile,
                 FitPrep pr) {
     if (quad) {
-        const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks), b(64 * FARMS_FIT_WPB);
+        const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks), b(64);
         switch (fr) {
         case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq, pr); return true;
         case 2:
@@ -2606,33 +2430,6 @@ int ensure_sync_events(farms_handle *h, size_t count) {
     return FARMS_OK;
 }
 
-// FARMS_GRAPH experiment aid: a SIGSEGV inside the graph runtime prints the
-// host call stack (on an alternate signal stack: the fault may be a stack
-// overflow) before the process dies.
-static void graph_segv_handler(int sig) {
-    void *fr[48];
-    const int k = backtrace(fr, 48);
-    static const char msg[] = "[farms graph] SIGSEGV, host stack:\n";
-    (void)!write(2, msg, sizeof(msg) - 1);
-    backtrace_symbols_fd(fr, k, 2);
-    signal(sig, SIG_DFL);
-    raise(sig);
-}
-static void graph_segv_trace() {
-    static bool done = false;
-    if (done) return;
-    done = true;
-    static std::vector<char> alt(1 << 16);
-    stack_t ss{};
-    ss.ss_sp = alt.data();
-    ss.ss_size = alt.size();
-    sigaltstack(&ss, nullptr);
-    struct sigaction sa{};
-    sa.sa_handler = graph_segv_handler;
-    sa.sa_flags = SA_ONSTACK;
-    sigaction(SIGSEGV, &sa, nullptr);
-}
-
 // The whole per-event loop for n device-resident events.  on_super (may be
 // null) is called as soon as the work of pooling super-chunk S (events [p0,
 // p1)) is enqueued, with the event that marks its records final on the device:
@@ -2645,6 +2442,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
              int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0) {
     const int n = (int)n64;
     hipStream_t s = h->stream;
+    h->fresh = false;
     Ctx c{};
     c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH; c.WHs = (int64_t)h->W * h->H;
     c.X0 = h->X0; c.XR1 = h->X0 + h->WR; c.own_lo = h->own_lo; c.own_hi = h->own_hi;
@@ -2673,14 +2471,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.counters = h->counters;
     c.dbg_tc = h->counting ? h->dbg_tc : nullptr;
 
-    // FARMS_GRAPH=1 (experiment): the two sweeps of a plain call are
-    // captured into a hipGraph, instantiated and launched once (no timing events).
-    // Not under HIP runtimes before 7.2 (PyTorch 2.10 bundles 7.0): their stream
-    // capture recurses without bound on this launch pattern.
-    static const int hip_rt = [] { int v = 0; return hipRuntimeGetVersion(&v) == hipSuccess ? v : 0; }();
-    const char *gm = getenv("FARMS_GRAPH");
-    const bool graph = gm && gm[0] == '1' && phase == 0 && !on_super && hip_rt >= 70200000;
-    const bool prof = h->profiling && !graph;
+    const bool prof = h->profiling;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
     const int B = h->pool_batch;
     const int n_super = ceil_div(n_pool_chunks, B);
@@ -2762,7 +2553,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     auto prep_of = [&](int f) {  // the prep of chunk f (into buffer f % 2); blocks for 64-thread blocks
         FitPrep pr{cells_of(f), fit_start(std::max(f - 2, 0)), fit_start(f), fit_chunk_end(f), seq_base + f + 1, 0};
         pr.blocks = ceil_div(std::max(pr.c1 - pr.c0, pr.c0 - pr.p0), 64);
-        if (FARMS_FIT_PREP_FIRST) pr.blocks = (pr.blocks + 7) & ~7;  // whole rounds of the 8 XCDs
         return pr;
     };
     auto launch_prep = [&](const FitPrep &pr) {
@@ -2799,14 +2589,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         }
         return FARMS_OK;
     };
-    if (graph) graph_segv_trace();
-    if (graph && !serial) {  // the chain and pooling streams join the capture by a fork event on F
-        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        HIPCHK(hipEventRecord(ev_prep, s));
-        HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
-    } else if (graph) {
-        HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    }
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     int fit_enqueued = 0, fit_waited = -1;
     if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
@@ -2844,8 +2626,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
         for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
-            hipLaunchKernelGGL(k_chain, dim3(ceil_div(h->nblk, FARMS_CHAIN_WPB)), dim3(64 * FARMS_CHAIN_WPB), 0, sc, c, a,
-                               std::min(a + 64, ch1));
+            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1));
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
@@ -2875,26 +2656,6 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     if (n_super > 0) {
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
-    }
-    if (graph) {
-        std::fprintf(stderr, "[farms graph] enqueued; ending the capture\n");
-        const auto g0 = std::chrono::steady_clock::now();
-        hipGraph_t gr = nullptr;
-        HIPCHK(hipStreamEndCapture(s, &gr));
-        const auto g1 = std::chrono::steady_clock::now();
-        hipGraphExec_t ge = nullptr;
-        HIPCHK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
-        const auto g2 = std::chrono::steady_clock::now();
-        HIPCHK(hipGraphLaunch(ge, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const auto g3 = std::chrono::steady_clock::now();
-        size_t nodes = 0;
-        HIPCHK(hipGraphGetNodes(gr, nullptr, &nodes));
-        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        std::fprintf(stderr, "[farms graph] nodes %zu end_capture %.3f ms instantiate %.3f ms launch+run %.3f ms\n",
-                     nodes, ms(g0, g1), ms(g1, g2), ms(g2, g3));
-        HIPCHK(hipGraphExecDestroy(ge));
-        HIPCHK(hipGraphDestroy(gr));
     }
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (h->counting) {
@@ -2969,6 +2730,23 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         return fail(FARMS_EINVAL, "stored region outside the sensor");
     if (prm->own_x1 < 0 || (prm->own_x1 > 0 && (prm->own_x0 < 0 || prm->own_x0 >= prm->own_x1 || prm->own_x1 > prm->width)))
         return fail(FARMS_EINVAL, "bad owned column range");
+    if (prm->own_x1 > 0 && prm->region_width > 0) {
+        // the stored region must hold every column the owned events read: the
+        // pooling window (M left, M + the W-1 clip's alias columns right,
+        // vFlow.cpp:1000/1113) and, for fitted events, the SAE window (2 fRad,
+        // vFlow.cpp:870-883) -- of the halo events too unless their flows are
+        // imported
+        int fs = prm->filter_size;
+        if (fs < 5) fs = 3;
+        if (!(fs % 2)) fs--;
+        const int sae = 2 * (fs / 2), M = std::max(prm->max_window, 0);
+        const int alias = std::min(prm->height - 1 + M, prm->width - 1) / prm->height;
+        const int left = prm->import_halo ? std::max(M, sae) : M + sae;
+        const int right = prm->import_halo ? std::max(M + alias, sae) : M + alias + sae;
+        if (prm->region_x0 > std::max(0, prm->own_x0 - left) ||
+            prm->region_x0 + prm->region_width < std::min(prm->width, prm->own_x1 + right))
+            return fail(FARMS_EINVAL, "stored region does not cover the owned columns' halo");
+    }
     const int K = prm->max_window / prm->window_jump + 1;
     // spatialPool has maxWindow slots and is indexed with .at() (vFlow.cpp:966,1025)
     if (K > prm->max_window) return fail(FARMS_EINVAL, "more pooling scales than maxWindow (reference throws)");
@@ -3015,7 +2793,6 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->cstride = (int64_t)h->nblk * kGroupCells;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
-    if (const char *v = getenv("FARMS_POOL_TILE")) h->tile_shift = std::max(1, std::min(atoi(v), 6));
     {
         const int tm = (1 << h->tile_shift) - 1;
         const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);
@@ -3025,35 +2802,14 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     auto bail = [&](int code) { farms_destroy(h); return code; };
     // the fit sweep and the candidate chain are the latency-critical dependency
     // path: high priority; the bulk pooling launches fill the remaining CUs
+    // (measured and rejected: a CU mask keeping pooling waves off some CUs of
+    // each XCD, other priority assignments: DESIGN.md §8)
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    // FARMS_STREAM_PRIO = three digits (fit, chain, pool), 1 = high: tuning aid
-    int pr[3] = {prio_hi, prio_hi, prio_lo};
-    if (const char *sp = getenv("FARMS_STREAM_PRIO"))
-        for (int i = 0; i < 3 && sp[i]; ++i) pr[i] = sp[i] == '1' ? prio_hi : prio_lo;
-    if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, pr[0]) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, pr[1]) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, pr[2]) != hipSuccess)
+    if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
-    // FARMS_POOL_CU_SKIP = k (0..4): k CUs per XCD left out of the pooling
-    // stream's CU mask, so the fit chain always finds free slots there.  Bits
-    // 32j + 8t + j (t < k): k per 32-bit word and k per residue mod 8, whichever
-    // way the mask bits map to XCDs.
-    if (const char *v = getenv("FARMS_POOL_CU_SKIP")) {
-        const int k = std::max(0, std::min(atoi(v), 4));
-        int dev = 0;
-        hipDeviceProp_t dp{};
-        if (k > 0 && hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&dp, dev) == hipSuccess &&
-            dp.multiProcessorCount % 32 == 0) {
-            const int ncu = dp.multiProcessorCount;
-            std::vector<uint32_t> m((size_t)ncu / 32, 0xffffffffu);
-            for (int j = 0; j < ncu / 32; ++j)
-                for (int t = 0; t < k; ++t) m[j] &= ~(1u << (8 * t + (j & 7)));
-            if (hipStreamDestroy(h->s_pool) != hipSuccess ||
-                hipExtStreamCreateWithCUMask(&h->s_pool, (uint32_t)m.size(), m.data()) != hipSuccess)
-                return bail(fail(FARMS_EHIP, "hipExtStreamCreateWithCUMask"));
-        }
-    }
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
@@ -3124,12 +2880,12 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
     (void)hipFree(d);
     // serial mode: the first line stamps lastEventTime without entering the SAE
-    // (vFlow.cpp:556); it shows until an event fires at that pixel
-    if (h->first_q >= 0 && out[h->first_q] == 0.0) {
-        FlowCell f{};
-        if (hipMemcpy(&f, h->fsnap + (h->first_q - (int64_t)h->X0 * h->H), sizeof(f), hipMemcpyDeviceToHost) == hipSuccess &&
-            f.t == h->first_t)
-            out[h->first_q] = (double)h->first_t;
+    // (vFlow.cpp:556); it shows until an event fires at that pixel (which marks
+    // the pixel's SAE cell visited)
+    if (err == hipSuccess && h->first_q >= 0) {
+        SaeCell cell{};
+        err = hipMemcpy(&cell, h->cells + (h->first_q - (int64_t)h->X0 * h->H), sizeof(cell), hipMemcpyDeviceToHost);
+        if (err == hipSuccess && !(cell.tag >> 31)) out[h->first_q] = (double)h->first_t;
     }
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
     return FARMS_OK;
@@ -3183,6 +2939,7 @@ extern "C" int farms_seed_sae(farms_handle *h, const int64_t *d_stamp) {
 extern "C" int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_t t_abs) {
     if (!h) return fail(FARMS_EINVAL, "null handle");
     if (!h->prm.serial) return fail(FARMS_EINVAL, "farms_serial_first needs a serial-mode handle");
+    if (!h->fresh) return fail(FARMS_EINVAL, "farms_serial_first after events: reset the handle first");
     if (x < h->X0 || x >= h->X0 + h->WR || y < 0 || y >= h->H) return fail(FARMS_EINVAL, "event outside the sensor");
     HIPCHK(hipSetDevice(h->prm.device));
     const int64_t q = (int64_t)(x - h->X0) * h->H + y;
@@ -3260,6 +3017,7 @@ extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t
 extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
                                     const uint32_t *d_t, const int32_t *d_p, int64_t n, farms_records *d_out) {
     if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
+    if (h->prm.import_halo) return fail(FARMS_EINVAL, "an import_halo handle runs farms_fit_device / farms_pool_device");
     if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
     if (n == 0) return FARMS_OK;
     if (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx || !d_out->vy ||
@@ -3306,6 +3064,7 @@ int ensure_pinned(farms_handle *h, int64_t n) {
 extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
+    if (h->prm.import_halo) return fail(FARMS_EINVAL, "an import_halo handle runs farms_fit_device / farms_pool_device");
     if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
     if (n == 0) return FARMS_OK;
     if (!x || !y || !t || !p || !out->x || !out->y || !out->t || !out->p || !out->r_true || !out->theta_true ||

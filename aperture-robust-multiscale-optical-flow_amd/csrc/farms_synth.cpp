@@ -7,7 +7,13 @@
 // PRNG: SplitMix64 (Steele, Lea, Flood 2014):
 //   s += 0x9E3779B97F4A7C15; z = s; z = (z ^ z>>30) * 0xBF58476D1CE4E5B9;
 //   z = (z ^ z>>27) * 0x94D049BB133111EB; return z ^ z>>31;
-// uniform double = (z >> 11) * 2^-53.
+// uniform double = (z >> 11) * 2^-53.  The bars' parameters come from one
+// SplitMix64 sequence seeded with `seed`.  Every per-event draw is counter-based
+// instead -- the SplitMix64 output function of a hash of the event's identity
+// (time step, bar, pixel, edge crossing; noise event number) -- so any block of
+// time steps can be generated on its own: blocks run on parallel threads, and a
+// rank's share [e0, e1) of a long stream is produced without materialising the
+// rest (two passes: per-microsecond counts, then the keys of the window).
 //
 // Geometry: pixel (px, py) has its centre at (px, py).  A bar is the rectangle
 // |(q-c).u| <= L/2, |(q-c).m| <= w/2 with u the long axis and m its normal.  The
@@ -16,13 +22,20 @@
 // of its swept parallelogram are visited by scanline and the exact entry (ON,
 // p=+1) / exit (OFF, p=-1) instant of each pixel centre is solved from the two
 // slab intervals; an event is emitted by the edge that binds it, so corners are
-// not duplicated.
+// not duplicated.  The signal is simulated step by step until it holds
+// n_signal + n_signal/64 + 1024 events (a margin for the tail cut), noise is
+// spread uniformly over the simulated span, and the stream is the first
+// n_events events in (t, x, y, p) order.
 #include "../../include/farms_synth.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -39,12 +52,20 @@ struct SplitMix64 {
     }
     double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
     double uniform(double a, double b) { return a + (b - a) * uniform(); }
-    uint64_t below(uint64_t n) { return n ? next() % n : 0; }
 };
 
+// SplitMix64's output function: the counter-based draw of a hashed identity.
+inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 constexpr double kPi = 3.14159265358979323846;
-constexpr double kStepUs = 100.0;  // motion is linear within a step
+constexpr uint32_t kStepUs = 100;  // motion is linear within a step
 constexpr double kStepS = kStepUs * 1e-6;
+constexpr int kBlockSteps = 64;    // time steps per generation block (one thread's unit)
 
 struct Bar {
     double cx, cy, vx, vy;  // centre (px) and velocity (px/s)
@@ -59,6 +80,7 @@ inline uint64_t make_key(uint32_t t, int x, int y, int p) {
     return ((uint64_t)t << 32) | ((uint64_t)(uint32_t)x << 16) | ((uint64_t)(uint32_t)y << 1) |
            (uint64_t)(p > 0 ? 1 : 0);
 }
+inline int key_x(uint64_t k) { return (int)((k >> 16) & 0xFFFF); }
 
 void radix_sort_u64(std::vector<uint64_t> &a) {
     std::vector<uint64_t> tmp(a.size());
@@ -89,11 +111,15 @@ inline bool slab(double a0, double v, double h, double &lo, double &hi, int &sid
     return true;
 }
 
-void emit_bar_step(const Bar &b, uint32_t step_t0_us, int W, int H, int jitter, SplitMix64 &rng,
-                   std::vector<uint64_t> &keys, uint32_t t0) {
+// The events of bar `bi` during time step `step`: sink(t_off, px, py, p) with
+// t_off the stamp minus t0 (us).  Jitter U{0..J}: a counter-based draw from
+// (seed, step, bar, pixel, entry/exit).
+template <class Sink>
+void emit_bar_step(const Bar &b, int bi, uint32_t step, int W, int H, int jitter, uint64_t seed, Sink &&sink) {
     const double vu = b.vx * b.ux + b.vy * b.uy;
     const double vm = b.vx * b.mx + b.vy * b.my;
     const V2 dv{b.vx * kStepS, b.vy * kStepS};
+    const uint64_t hstep = mix64(seed ^ (((uint64_t)step << 16) | (uint64_t)bi));
     // edges: (slab 0 = u, slab 1 = m) x (side +1, -1)
     for (int slab_id = 0; slab_id < 2; ++slab_id) {
         for (int side = +1; side >= -1; side -= 2) {
@@ -147,14 +173,267 @@ void emit_bar_step(const Bar &b, uint32_t step_t0_us, int W, int H, int jitter, 
                         if (!(tau >= 0.0 && tau < kStepS)) continue;
                         if ((which == 0 ? bind_lo : bind_hi) != slab_id) continue;
                         if ((which == 0 ? side_lo : side_hi) != side) continue;
-                        uint32_t tt = t0 + step_t0_us + (uint32_t)std::floor(tau * 1e6) +
-                                      (uint32_t)rng.below((uint64_t)jitter + 1);
-                        keys.push_back(make_key(tt, px, py, which == 0 ? +1 : -1));
+                        const uint64_t h = mix64(hstep ^ (((uint64_t)px << 17) | ((uint64_t)py << 1) | (uint64_t)which));
+                        const uint32_t tt = step * kStepUs + (uint32_t)std::floor(tau * 1e6) +
+                                            (uint32_t)(h % ((uint64_t)jitter + 1));
+                        sink(tt, px, py, which == 0 ? +1 : -1);
                     }
                 }
             }
         }
     }
+}
+
+void advance(std::vector<Bar> &bars, int W, int H) {
+    for (Bar &b : bars) {
+        b.cx += b.vx * kStepS;
+        b.cy += b.vy * kStepS;
+        if (b.cx < 0) { b.cx = -b.cx; b.vx = -b.vx; }
+        if (b.cx > W - 1) { b.cx = 2.0 * (W - 1) - b.cx; b.vx = -b.vx; }
+        if (b.cy < 0) { b.cy = -b.cy; b.vy = -b.vy; }
+        if (b.cy > H - 1) { b.cy = 2.0 * (H - 1) - b.cy; b.vy = -b.vy; }
+    }
+}
+
+int n_threads() {
+    // OMP_NUM_THREADS (16 on the GPU boxes, whose nproc shows the whole host) or
+    // the hardware count, at most 32
+    const char *v = std::getenv("FARMS_SYNTH_THREADS");
+    if (!v) v = std::getenv("OMP_NUM_THREADS");
+    int t = v ? std::atoi(v) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 32));
+}
+
+// fn(i) for i in [0, n) on the worker threads
+template <class Fn>
+void parallel_for(int64_t n, Fn &&fn) {
+    const int T = (int)std::min<int64_t>(n_threads(), std::max<int64_t>(n, 1));
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        for (int64_t i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; ++k) th.emplace_back(work);
+    work();
+    for (auto &w : th) w.join();
+}
+
+constexpr int64_t kNoiseChunk = 1 << 20;
+
+// The stream's plan (pass 1): bars, simulated step count, and the number of
+// events per microsecond of stamp offset and per column (before the tail cut).
+struct Stream {
+    farms_synth_params p{};
+    std::vector<Bar> bars;
+    int64_t n_noise = 0, n_signal = 0;
+    uint32_t steps = 0;        // signal time steps simulated
+    uint64_t span_us = 1;      // noise stamps are uniform in [0, span)
+    std::vector<uint32_t> ht;  // events per us offset (length: horizon)
+    std::vector<int64_t> hx;   // events per column
+    std::vector<int64_t> cum;  // cum[b] = events with t_off < b (length ht.size() + 1)
+    uint64_t noise_seed = 0;
+};
+
+inline void noise_event(const Stream &S, int64_t k, uint32_t &t_off, int &x, int &y, int &p) {
+    const uint64_t z = mix64(S.noise_seed + (uint64_t)k * 0xD1B54A32D192ED03ull);
+    t_off = (uint32_t)(z % S.span_us);
+    x = (int)(mix64(z ^ 1) % (uint64_t)S.p.width);
+    y = (int)(mix64(z ^ 2) % (uint64_t)S.p.height);
+    p = (mix64(z ^ 3) & 1) ? +1 : -1;
+}
+
+int plan_stream(const farms_synth_params *p, Stream &S) {
+    if (!p || p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 32767 ||
+        p->n_events < 0 || p->n_bars < 0 || p->noise_frac < 0 || p->noise_frac >= 1 || p->jitter_us < 0)
+        return -1;
+    if (p->n_events > 0 && p->n_bars == 0 && p->noise_frac <= 0) return -1;
+    S.p = *p;
+    const int W = p->width, H = p->height, J = p->jitter_us;
+    SplitMix64 rng(p->seed);
+    S.bars.resize((size_t)p->n_bars);
+    for (Bar &b : S.bars) {
+        b.cx = rng.uniform(0, W - 1);
+        b.cy = rng.uniform(0, H - 1);
+        double dir;
+        if (p->fixed_dir_deg >= 0) {
+            dir = p->fixed_dir_deg * kPi / 180.0;
+        } else {  // reject directions within 10 degrees of an axis (SURVEY §A Q5)
+            do { dir = rng.uniform(0, 2 * kPi); } while (std::fmod(dir, kPi / 2) < 10 * kPi / 180 ||
+                                                         std::fmod(dir, kPi / 2) > 80 * kPi / 180);
+        }
+        double speed = rng.uniform(p->speed_min, p->speed_max);
+        b.vx = speed * std::cos(dir);
+        b.vy = speed * std::sin(dir);
+        double axis = dir + kPi / 2 + (p->fixed_dir_deg >= 0 ? 0.0 : rng.uniform(-20, 20) * kPi / 180);
+        b.ux = std::cos(axis); b.uy = std::sin(axis);
+        b.mx = -b.uy; b.my = b.ux;
+        b.half_len = 0.5 * rng.uniform(p->len_min, p->len_max);
+        b.half_thick = 0.5 * rng.uniform(p->thick_min, p->thick_max);
+    }
+    S.noise_seed = rng.next();
+    S.n_noise = (int64_t)std::llround((double)p->n_events * p->noise_frac);
+    S.n_signal = p->n_events - S.n_noise;
+    S.hx.assign((size_t)W, 0);
+    S.ht.clear();
+    const int64_t target = S.n_signal > 0 && !S.bars.empty() ? S.n_signal + S.n_signal / 64 + 1024 : 0;
+    // signal: rounds of blocks of kBlockSteps steps on parallel threads, each
+    // with local per-step / per-us / per-column counts, merged in block order
+    // until the step where the simulated signal reaches the target
+    const int nb = 4 * n_threads();
+    const uint32_t blk_us = kBlockSteps * kStepUs + (uint32_t)J + 1;  // stamp offsets of one block
+    struct Blk {
+        uint32_t s0;
+        std::vector<Bar> st;
+        std::vector<int64_t> per_step, hx;
+        std::vector<uint32_t> ht;
+    };
+    std::vector<Blk> blk((size_t)nb);
+    auto count_block = [&](Blk &B, uint32_t s_end) {
+        B.per_step.assign(kBlockSteps, 0);
+        B.ht.assign(blk_us, 0);
+        B.hx.assign((size_t)W, 0);
+        std::vector<Bar> bars = B.st;
+        for (uint32_t s = B.s0; s < s_end; ++s) {
+            int64_t cnt = 0;
+            for (size_t bi = 0; bi < bars.size(); ++bi)
+                emit_bar_step(bars[bi], (int)bi, s, W, H, J, p->seed, [&](uint32_t tt, int px, int, int) {
+                    ++cnt;
+                    B.ht[tt - B.s0 * kStepUs]++;
+                    B.hx[(size_t)px]++;
+                });
+            B.per_step[s - B.s0] = cnt;
+            advance(bars, W, H);
+        }
+    };
+    std::vector<Bar> cur = S.bars;
+    int64_t have = 0;
+    uint32_t s_base = 0;
+    bool done = target == 0;
+    while (!done) {
+        if ((uint64_t)s_base + (uint64_t)nb * kBlockSteps > 4000000000ull / kStepUs) return -2;  // uint32 time
+        for (int i = 0; i < nb; ++i) {
+            blk[(size_t)i].s0 = s_base + (uint32_t)i * kBlockSteps;
+            blk[(size_t)i].st = cur;
+            for (int s = 0; s < kBlockSteps; ++s) advance(cur, W, H);
+        }
+        parallel_for(nb, [&](int64_t i) { count_block(blk[(size_t)i], blk[(size_t)i].s0 + kBlockSteps); });
+        for (int i = 0; i < nb && !done; ++i) {
+            Blk &B = blk[(size_t)i];
+            int s_stop = kBlockSteps;
+            for (int s = 0; s < kBlockSteps; ++s) {
+                have += B.per_step[(size_t)s];
+                if (have >= target) { s_stop = s + 1; done = true; break; }
+            }
+            if (s_stop < kBlockSteps) count_block(B, B.s0 + (uint32_t)s_stop);  // the last steps only
+            const size_t need = (size_t)B.s0 * kStepUs + blk_us;
+            if (S.ht.size() < need) S.ht.resize(need, 0);
+            for (uint32_t u = 0; u < blk_us; ++u) S.ht[(size_t)B.s0 * kStepUs + u] += B.ht[u];
+            for (int x = 0; x < W; ++x) S.hx[(size_t)x] += B.hx[(size_t)x];
+            S.steps = B.s0 + (uint32_t)s_stop;
+        }
+        s_base += (uint32_t)nb * kBlockSteps;
+    }
+    S.span_us = std::max<uint64_t>(1, (uint64_t)S.steps * kStepUs);
+    if (S.ht.size() < S.span_us) S.ht.resize(S.span_us, 0);
+    // noise: counter-based draws, counted with atomic adds
+    {
+        std::vector<std::atomic<int64_t>> hx(W);
+        for (auto &v : hx) v.store(0);
+        uint32_t *ht = S.ht.data();
+        const int64_t nchunks = (S.n_noise + kNoiseChunk - 1) / kNoiseChunk;
+        parallel_for(nchunks, [&](int64_t c) {
+            std::vector<int64_t> lx((size_t)W, 0);
+            const int64_t k1 = std::min(S.n_noise, (c + 1) * kNoiseChunk);
+            for (int64_t k = c * kNoiseChunk; k < k1; ++k) {
+                uint32_t t; int x, y, pp;
+                noise_event(S, k, t, x, y, pp);
+                __atomic_fetch_add(&ht[t], 1u, __ATOMIC_RELAXED);
+                lx[(size_t)x]++;
+            }
+            for (int x = 0; x < W; ++x) hx[(size_t)x].fetch_add(lx[(size_t)x]);
+        });
+        for (int x = 0; x < W; ++x) S.hx[(size_t)x] += hx[(size_t)x].load();
+    }
+    S.cum.assign(S.ht.size() + 1, 0);
+    for (size_t b = 0; b < S.ht.size(); ++b) S.cum[b + 1] = S.cum[b] + S.ht[b];
+    if (S.cum.back() < p->n_events) return -3;
+    return 0;
+}
+
+// Pass 2: the keys with stamp offset in [ta, tb] and column in [x_lo, x_hi),
+// sorted; below[t - ta] (if given) counts the events of that microsecond in
+// columns < x_lo.
+void collect(const Stream &S, uint32_t ta, uint32_t tb, int x_lo, int x_hi, std::vector<uint64_t> &keys,
+             std::vector<uint32_t> *below) {
+    const int W = S.p.width, H = S.p.height, J = S.p.jitter_us;
+    const uint32_t t0 = S.p.t0;
+    if (below) below->assign((size_t)(tb - ta) + 1, 0);
+    uint32_t *bl = below ? below->data() : nullptr;
+    auto keep = [&](std::vector<uint64_t> &out, uint32_t tt, int px, int py, int pol) {
+        if (tt < ta || tt > tb) return;
+        if (px < x_lo) {
+            if (bl) __atomic_fetch_add(&bl[tt - ta], 1u, __ATOMIC_RELAXED);
+            return;
+        }
+        if (px >= x_hi) return;
+        out.push_back(make_key(t0 + tt, px, py, pol));
+    };
+    const int64_t nblk = ((int64_t)S.steps + kBlockSteps - 1) / kBlockSteps;
+    const int64_t nchunks = (S.n_noise + kNoiseChunk - 1) / kNoiseChunk;
+    std::vector<std::vector<uint64_t>> part((size_t)(nblk + nchunks));
+    // bar states at each block start (sequential, cheap)
+    std::vector<std::vector<Bar>> st((size_t)nblk);
+    {
+        std::vector<Bar> cur = S.bars;
+        for (int64_t i = 0; i < nblk; ++i) {
+            st[(size_t)i] = cur;
+            for (int s = 0; s < kBlockSteps; ++s) advance(cur, W, H);
+        }
+    }
+    parallel_for(nblk + nchunks, [&](int64_t i) {
+        std::vector<uint64_t> &out = part[(size_t)i];
+        if (i < nblk) {
+            const uint32_t s0 = (uint32_t)i * kBlockSteps;
+            const uint32_t s1 = std::min<uint32_t>(S.steps, s0 + kBlockSteps);
+            if ((uint64_t)s0 * kStepUs > tb || (uint64_t)s1 * kStepUs + (uint64_t)J < ta) return;  // outside the window
+            std::vector<Bar> bars = st[(size_t)i];
+            for (uint32_t s = s0; s < s1; ++s) {
+                for (size_t bi = 0; bi < bars.size(); ++bi)
+                    emit_bar_step(bars[bi], (int)bi, s, W, H, J, S.p.seed,
+                                  [&](uint32_t tt, int px, int py, int pol) { keep(out, tt, px, py, pol); });
+                advance(bars, W, H);
+            }
+        } else {
+            const int64_t c = i - nblk;
+            const int64_t k1 = std::min(S.n_noise, (c + 1) * kNoiseChunk);
+            for (int64_t k = c * kNoiseChunk; k < k1; ++k) {
+                uint32_t t; int x, y, pp;
+                noise_event(S, k, t, x, y, pp);
+                keep(out, t, x, y, pp);
+            }
+        }
+    });
+    size_t total = 0;
+    for (auto &v : part) total += v.size();
+    keys.clear();
+    keys.reserve(total);
+    for (auto &v : part) {
+        keys.insert(keys.end(), v.begin(), v.end());
+        std::vector<uint64_t>().swap(v);
+    }
+    radix_sort_u64(keys);
+}
+
+inline void unpack(uint64_t k, int32_t &x, int32_t &y, uint32_t &t, int32_t &pol) {
+    t = (uint32_t)(k >> 32);
+    x = (int32_t)((k >> 16) & 0xFFFF);
+    y = (int32_t)((k >> 1) & 0x7FFF);
+    pol = (k & 1) ? 1 : -1;
+}
+
+// The microsecond bucket holding stream index e (0 <= e < cum.back()).
+uint32_t bucket_of(const Stream &S, int64_t e) {
+    return (uint32_t)(std::upper_bound(S.cum.begin(), S.cum.end(), e) - S.cum.begin() - 1);
 }
 
 }  // namespace
@@ -190,86 +469,10 @@ extern "C" int farms_synth_preset(int config, farms_synth_params *o) {
     }
 }
 
-namespace {
-
-// The whole stream as sorted keys (at least n_events of them), or a negative code.
-int64_t generate_keys(const farms_synth_params *p, std::vector<uint64_t> &keys) {
-    if (!p || p->width <= 0 || p->height <= 0 || p->width > 65535 || p->height > 32767 ||
-        p->n_events < 0 || p->n_bars < 0 || p->noise_frac < 0 || p->noise_frac >= 1)
-        return -1;
-    if (p->n_events == 0) return 0;
-    if (p->n_bars == 0 && p->noise_frac <= 0) return -1;
-    const int W = p->width, H = p->height;
-    SplitMix64 rng(p->seed);
-    std::vector<Bar> bars((size_t)p->n_bars);
-    for (Bar &b : bars) {
-        b.cx = rng.uniform(0, W - 1);
-        b.cy = rng.uniform(0, H - 1);
-        double dir;
-        if (p->fixed_dir_deg >= 0) {
-            dir = p->fixed_dir_deg * kPi / 180.0;
-        } else {  // reject directions within 10 degrees of an axis (SURVEY §A Q5)
-            do { dir = rng.uniform(0, 2 * kPi); } while (std::fmod(dir, kPi / 2) < 10 * kPi / 180 ||
-                                                         std::fmod(dir, kPi / 2) > 80 * kPi / 180);
-        }
-        double speed = rng.uniform(p->speed_min, p->speed_max);
-        b.vx = speed * std::cos(dir);
-        b.vy = speed * std::sin(dir);
-        double axis = dir + kPi / 2 + (p->fixed_dir_deg >= 0 ? 0.0 : rng.uniform(-20, 20) * kPi / 180);
-        b.ux = std::cos(axis); b.uy = std::sin(axis);
-        b.mx = -b.uy; b.my = b.ux;
-        b.half_len = 0.5 * rng.uniform(p->len_min, p->len_max);
-        b.half_thick = 0.5 * rng.uniform(p->thick_min, p->thick_max);
-    }
-    const int64_t n_noise = (int64_t)std::llround((double)p->n_events * p->noise_frac);
-    const int64_t n_signal = p->n_events - n_noise;
-    keys.clear();
-    keys.reserve((size_t)(p->n_events + p->n_events / 16 + 4096));
-    // simulate until the signal budget (plus a margin for the tail cut) is reached
-    const int64_t margin = n_signal / 64 + 1024;
-    uint32_t step = 0;
-    if (n_signal > 0 && !bars.empty()) {
-        while ((int64_t)keys.size() < n_signal + margin) {
-            for (Bar &b : bars) {
-                emit_bar_step(b, step * (uint32_t)kStepUs, W, H, p->jitter_us, rng, keys, p->t0);
-                b.cx += b.vx * kStepS;
-                b.cy += b.vy * kStepS;
-                if (b.cx < 0) { b.cx = -b.cx; b.vx = -b.vx; }
-                if (b.cx > W - 1) { b.cx = 2.0 * (W - 1) - b.cx; b.vx = -b.vx; }
-                if (b.cy < 0) { b.cy = -b.cy; b.vy = -b.vy; }
-                if (b.cy > H - 1) { b.cy = 2.0 * (H - 1) - b.cy; b.vy = -b.vy; }
-            }
-            ++step;
-            if (step > 4000000000u / (uint32_t)kStepUs) return -2;  // would overflow uint32 time
-        }
-    }
-    const uint64_t span_us = std::max<uint64_t>(1, (uint64_t)step * (uint64_t)kStepUs);
-    for (int64_t k = 0; k < n_noise; ++k) {
-        uint32_t tt = p->t0 + (uint32_t)rng.below(span_us);
-        int nx = (int)rng.below((uint64_t)W), ny = (int)rng.below((uint64_t)H);
-        keys.push_back(make_key(tt, nx, ny, (rng.next() & 1) ? +1 : -1));
-    }
-    radix_sort_u64(keys);
-    if ((int64_t)keys.size() < p->n_events) return -3;
-    return p->n_events;
-}
-
-inline void unpack(uint64_t k, int32_t &x, int32_t &y, uint32_t &t, int32_t &pol) {
-    t = (uint32_t)(k >> 32);
-    x = (int32_t)((k >> 16) & 0xFFFF);
-    y = (int32_t)((k >> 1) & 0x7FFF);
-    pol = (k & 1) ? 1 : -1;
-}
-
-}  // namespace
-
 extern "C" int64_t farms_synth_generate(const farms_synth_params *p, int32_t *x, int32_t *y,
                                         uint32_t *t, int32_t *pol) {
-    std::vector<uint64_t> keys;
-    const int64_t n = generate_keys(p, keys);
-    if (n <= 0) return n;
-    for (int64_t e = 0; e < n; ++e) unpack(keys[(size_t)e], x[e], y[e], t[e], pol[e]);
-    return n;
+    return farms_synth_generate_select(p, 0, p ? p->n_events : 0, 0, p ? p->width : 0, p ? p->n_events : 0, x, y, t,
+                                       pol, nullptr, nullptr);
 }
 
 extern "C" int64_t farms_synth_generate_select(const farms_synth_params *p, int64_t e0, int64_t e1,
@@ -277,21 +480,38 @@ extern "C" int64_t farms_synth_generate_select(const farms_synth_params *p, int6
                                                int32_t *y, uint32_t *t, int32_t *pol, int64_t *idx,
                                                uint32_t *t_first) {
     if (!p || e0 < 0 || e1 < e0 || cap < 0 || (cap > 0 && (!x || !y || !t || !pol))) return -1;
-    std::vector<uint64_t> keys;
-    const int64_t n = generate_keys(p, keys);
-    if (n < 0) return n;
-    if (t_first) *t_first = n > 0 ? (uint32_t)(keys[0] >> 32) : 0u;
+    Stream S;
+    int rc = plan_stream(p, S);
+    if (rc) return rc;
+    const int64_t n = p->n_events;
+    if (t_first) *t_first = n > 0 ? p->t0 + bucket_of(S, 0) : 0u;
     if (e1 > n) e1 = n;
+    x_lo = std::max(x_lo, 0);
+    x_hi = std::min(x_hi, p->width);
+    if (e0 >= e1 || x_lo >= x_hi) return 0;
+    const uint32_t ta = bucket_of(S, e0), tb = bucket_of(S, e1 - 1);
+    const bool all_cols = x_lo == 0 && x_hi == p->width;
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> below;
+    collect(S, ta, tb, x_lo, x_hi, keys, all_cols ? nullptr : &below);
+    // stream index of each kept key: the events of earlier microseconds, the
+    // earlier columns of its own microsecond, its rank among the kept ones
     int64_t m = 0;
-    for (int64_t e = e0; e < e1; ++e) {
-        const uint64_t k = keys[(size_t)e];
-        const int32_t kx = (int32_t)((k >> 16) & 0xFFFF);
-        if (kx < x_lo || kx >= x_hi) continue;
-        if (m < cap) {
-            unpack(k, x[m], y[m], t[m], pol[m]);
-            if (idx) idx[m] = e;
+    size_t k = 0;
+    while (k < keys.size()) {
+        const uint32_t b = (uint32_t)(keys[k] >> 32) - p->t0;
+        const int64_t base = S.cum[b] + (all_cols ? 0 : (int64_t)below[b - ta]);
+        size_t j = k;
+        for (; j < keys.size() && (uint32_t)(keys[j] >> 32) - p->t0 == b; ++j) {
+            const int64_t e = base + (int64_t)(j - k);
+            if (e < e0 || e >= e1) continue;
+            if (m < cap) {
+                unpack(keys[j], x[m], y[m], t[m], pol[m]);
+                if (idx) idx[m] = e;
+            }
+            ++m;
         }
-        ++m;
+        k = j;
     }
     return m;
 }
@@ -312,10 +532,18 @@ extern "C" int farms_synth_write_text(const char *path, const int32_t *x, const 
 
 extern "C" int farms_synth_column_hist(const farms_synth_params *p, int64_t *hist) {
     if (!p || !hist) return -1;
-    std::vector<uint64_t> keys;
-    const int64_t n = generate_keys(p, keys);
-    if (n < 0) return (int)n;
-    std::memset(hist, 0, sizeof(int64_t) * (size_t)p->width);
-    for (int64_t e = 0; e < n; ++e) hist[(keys[(size_t)e] >> 16) & 0xFFFF]++;
+    Stream S;
+    int rc = plan_stream(p, S);
+    if (rc) return rc;
+    for (int x = 0; x < p->width; ++x) hist[x] = S.hx[(size_t)x];
+    // minus the tail cut: events with stream index >= n_events
+    const int64_t n = p->n_events, total = S.cum.back();
+    if (total > n) {
+        const uint32_t ta = bucket_of(S, n), tb = (uint32_t)S.ht.size() - 1;
+        std::vector<uint64_t> keys;
+        collect(S, ta, tb, 0, p->width, keys, nullptr);
+        for (size_t j = 0; j < keys.size(); ++j)
+            if (S.cum[ta] + (int64_t)j >= n) hist[key_x(keys[j])]--;
+    }
     return 0;
 }

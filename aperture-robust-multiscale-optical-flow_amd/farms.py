@@ -268,14 +268,17 @@ def synth_generate(params: SynthParams) -> Events:
     return Events(x, y, t, p)
 
 
-def synth_select(params: SynthParams, e0: int, e1: int, x_lo: int = 0, x_hi: int | None = None):
+def synth_select(params: SynthParams, e0: int, e1: int, x_lo: int = 0, x_hi: int | None = None,
+                 count: int | None = None):
     """Events [e0, e1) of the stream with column in [x_lo, x_hi), their stream
     indices and the stream's first stamp, without materialising the whole
-    stream (farms_synth_generate_select): one rank's share."""
+    stream (farms_synth_generate_select): one rank's share.  `count`: the
+    number of matching events when known (from synth_column_hist), else the
+    arrays are sized for e1 - e0."""
     lib = load_synth_library()
     x_hi = int(params.width) if x_hi is None else int(x_hi)
     e1 = min(int(e1), int(params.n_events))
-    cap = max(e1 - int(e0), 0)
+    cap = max(e1 - int(e0), 0) if count is None else int(count)
     x = np.empty(cap, np.int32)
     y = np.empty(cap, np.int32)
     t = np.empty(cap, np.uint32)
@@ -285,8 +288,8 @@ def synth_select(params: SynthParams, e0: int, e1: int, x_lo: int = 0, x_hi: int
     got = lib.farms_synth_generate_select(ctypes.byref(params), ctypes.c_int64(int(e0)), ctypes.c_int64(e1),
                                           ctypes.c_int32(int(x_lo)), ctypes.c_int32(x_hi), ctypes.c_int64(cap),
                                           _ptr(x), _ptr(y), _ptr(t), _ptr(p), _ptr(idx), ctypes.byref(t_first))
-    if got < 0 or got > cap:
-        raise RuntimeError(f"farms_synth_generate_select returned {got}")
+    if got < 0 or got > cap or (count is not None and got != cap):
+        raise RuntimeError(f"farms_synth_generate_select returned {got} (expected {cap})")
     return Events(x[:got].copy(), y[:got].copy(), t[:got].copy(), p[:got].copy()), idx[:got].copy(), int(t_first.value)
 
 

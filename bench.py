@@ -5,17 +5,20 @@ Metric (BASELINE.json): Mevents/s (and % of the HBM roofline) at 1/2/4/8 GPUs.
 Workload at N=1: BASELINE config 3 — synthetic 1280x720 DVS-shape stream, 50M
 events, filtersize 5, inlierCheck 5 (the north_star's headline configuration).
 A step = one full pass of the hot path (surfaces reset + every event through
-local fit and multiscale pooling) over the whole resident stream.
+local fit and multiscale pooling) over the whole stream, resident in HBM when
+the timed region starts (the contract); the host-to-host rate of the C ABI
+(farms_process: H2D, kernels, D2H — SURVEY §8d's timed region) is reported
+beside it as `host_path`.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling — the stream holds N x
-the per-GPU event count on the same sensor.  On a time-ordered stream (the
-synthetic one is) rank r owns the r-th temporal segment: every step the ranks
-compute their per-pixel last-stamp surfaces on the GPU, all-gather them over
-RCCL, and each rank starts from the merged SAE plus a re-fitted 500 us warm-up
-(segments.py).  --split strips (or an unordered stream) uses
-x-strips with recomputed halos instead (strips.py).  Either way the owned
-records are bitwise those of a one-GPU run; value = owned events of all ranks
-/ max-over-ranks time.
+Multi-GPU (one process per GPU over RCCL; multirank.py): weak
+scaling — the stream holds N x the per-GPU event count on the same sensor.
+--split segments (default): rank r owns the r-th temporal segment, started
+every step from the SAE all-gathered over RCCL plus a re-fitted 500 us
+warm-up; --split strips: rank r owns an x-strip, fits its columns and
+exchanges the local flows of its halo events with one grouped send/recv per
+step.  Either way the owned records are bitwise those of a one-GPU run (the
+line's parity block checks that across every rank boundary on a short
+stream); value = owned events of all ranks / max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -27,6 +30,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -36,12 +40,20 @@ sys.path.insert(0, PKG)
 import numpy as np  # noqa: E402
 
 import farms  # noqa: E402
-import segments  # noqa: E402
-import strips  # noqa: E402
+import multirank  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720), 4: (1280, 720), 5: (1280, 720)}
 FILTER = {1: 3, 2: 5, 3: 5, 4: 7, 5: 7}
+# events per GPU, the weak-scaling unit: BASELINE.json config 4 is 200M events
+# on 4 GPUs, config 5 1G events on 8 GPUs; configs 1-3 run their own streams
+PER_GPU = {4: 50_000_000, 5: 125_000_000}
+METRIC = "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref"
+
+
+def scales(cfg: int) -> tuple[int, int]:
+    """(windowJump, maxWindow): config 5 pools 3 scales {0, 25, 50}."""
+    return (25, 50) if cfg == 5 else (5, 50)
 
 
 def parse():
@@ -50,15 +62,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--events", type=int, default=0, help="override the stream length")
+    ap.add_argument("--events", type=int, default=0, help="override the per-GPU stream length")
     ap.add_argument("--fit-chunk", type=int, default=0)
     ap.add_argument("--pool-chunk", type=int, default=0)
     ap.add_argument("--pool-batch", type=int, default=0, help="pooling chunks per k_pool launch (0 = engine default)")
     ap.add_argument("--cpu-sample", type=int, default=1_500_000, help="events in the CPU-baseline sample")
-    ap.add_argument("--parity-sample", type=int, default=300_000,
-                    help="N > 1: rank 0 checks its records of the stream's first K events against the oracle")
+    ap.add_argument("--parity-per-rank", type=int, default=60_000,
+                    help="N > 1: events per rank of the short stream whose merged records are checked against "
+                         "the oracle before the timed steps (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split", choices=("segments", "strips", "strips-recompute"), default="segments",
+    ap.add_argument("--split", choices=multirank.SPLITS, default="segments",
                     help="N > 1: temporal segments (time-ordered streams), x-strips with an RCCL exchange of "
                          "halo flows, or x-strips that recompute their halos")
     ap.add_argument("--host-steps", type=int, default=2,
@@ -85,27 +98,27 @@ def launch_ranks(n: int) -> int:
     return subprocess.run(cmd).returncode
 
 
-def cpu_baseline(sample, width, height, fs, jump, maxw):
-    """Oracle ("port": single-thread C restatement, -O2) on a head sample of the
-    same stream."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "unknown")
+    except OSError:
+        return "unknown"
+
+
+def cpu_baseline(x, y, t, p, k, width, height, fs, jump, maxw):
+    """Oracle ("port": single-thread C restatement, -O2) on the first k events
+    of the same stream."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import OracleFlow
 
-    x, y, t, p = sample.relative()
     of = OracleFlow(height, width, fs, 5, jump, maxw)
     t0 = time.perf_counter()
-    ref = of.process(x, y, t, p)
+    ref = of.process(x[:k], y[:k], t[:k], p[:k])
     dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu)
-    except OSError:
-        pass
-    return ref, {"value": len(sample) / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
-                 "sample": f"first {len(sample)} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, "
-                           f"{dt:.1f} s",
-                 "cpu_model": cpu, "host_threads": os.cpu_count()}
+    return ref, {"value": k / dt / 1e6, "unit": "Mevents/s", "cores": 1, "kind": "port",
+                 "sample": f"first {k} events of the same stream, oracle/farms_oracle.c -O2, 1 thread, {dt:.1f} s",
+                 "cpu_model": cpu_model(), "host_threads": os.cpu_count()}
 
 
 def parity_vs_cpu(ref, out, k):
@@ -150,12 +163,14 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
     FETCH_SIZE + WRITE_SIZE, the gfx950 correction) / the launch's average
     duration, timed live with HIP events on the pooling stream; frac = achieved
     / 8 TB/s.  The kernel is not HBM-bound (it reads a chunk's candidate lists
-    from L2): `issue` gives the bound that binds, from the SQ counters of the
-    same workload (VALU issue utilisation, waits).  SURVEY §8d's dense-window
-    figure (20 B per window cell of a valid event) is reported apart as
-    dense_equiv_*: the kernel never reads the dense window, so that figure
-    divided by the time exceeds HBM peak and is no physical rate."""
-    kname = "k_pool<11>" if cfg != 5 else "k_pool<3>"
+    from L2): `binds` names what binds, latency, and `issue` gives its
+    measures from the SQ counters of the same workload (VALU issue
+    utilisation, wait fractions).  SURVEY §8d's dense-window figure (20 B per
+    window cell of a valid event) is reported apart as dense_equiv_*: the
+    kernel never reads the dense window, so that figure divided by the time
+    exceeds HBM peak and is no physical rate."""
+    jump, maxw = scales(cfg)
+    kname = f"k_pool<{maxw // jump + 1}>"
     tr = committed_profile("traffic", cfg, world, pool_launches, kname)
     sq = committed_profile("sq", cfg, world, pool_launches, kname)
     traffic = round(tr["traffic_bytes_per_launch"]) if tr else None
@@ -166,53 +181,24 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
          "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
          "traffic_source": tr["source"] if tr else None,
          "kernel": "k_pool", "launches_per_step": pool_launches, "avg_launch_us": round(avg_us, 2),
+         "binds": "latency (dependent L2 loads and the fp64 fold chain), not HBM: see issue",
          "dense_equiv_bytes_per_launch": round(dense_per_launch),
          "dense_equiv_GBps": round(dense_per_launch / (avg_us * 1e-6) / 1e9, 1) if avg_us > 0 else None}
     if sq and avg_us > 0:
         waves = max(sq["SQ_WAVES"], 1.0)
         wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
         # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; a wave64
-        # VALU instruction occupies a SIMD-32 for 2 of them (fp64 FMA: 4), so
-        # this utilisation is a lower bound of the VALU pipe's busy fraction
+        # VALU instruction occupies a SIMD-32 for 2 of them (fp64: 4), so this
+        # utilisation is a lower bound of the VALU pipe's busy fraction
         simd_cycles = 1024 * 2.4e9 * avg_us * 1e-6
         r["issue"] = {"valu_insts_per_wave": round(sq["SQ_INSTS_VALU"] / waves, 1),
                       "valu_issue_util": round(2.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
-                      "binds": "latency: waves wait on dependent L2 loads and on the fp64 fold chain "
-                               "(wait_any + wait_inst > active); not HBM, not VALU throughput",
                       "wait_any_frac": round(sq["SQ_WAIT_ANY"] / wave_cyc, 4),
                       "wait_inst_frac": round(sq["SQ_WAIT_INST_ANY"] / wave_cyc, 4),
                       "active_inst_frac": round(sq["SQ_ACTIVE_INST_ANY"] / wave_cyc, 4),
                       "source": sq["source"]}
+        r["issue_frac"] = r["issue"]["valu_issue_util"]
     return r
-
-
-def parity_multi(args, cfg: int, sh: dict, out, owned_mask) -> dict:
-    """N > 1, rank 0: its owned records among the stream's first K events
-    against the oracle run on that prefix (the path is causal: a prefix of the
-    whole run equals a run of the prefix).  Exercises the exchange: rank 0's
-    records read halo flows (strips) or are checked across its segment's end."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle import OracleFlow
-    from parity import compare
-
-    W, H = SENSOR[cfg]
-    jump, maxw = (25, 50) if cfg == 5 else (5, 50)
-    sp = farms.synth_params(cfg)
-    sp.n_events = sh["n_stream"]
-    k = min(args.parity_sample, sh["n_stream"])
-    ev, _, t_first = farms.synth_select(sp, 0, k)
-    x, y, t, p = ev.relative(t_first)
-    ref = OracleFlow(H, W, FILTER[cfg], 5, jump, maxw).process(x, y, t, p)
-    sel = np.flatnonzero(owned_mask & (sh["gidx"] < k))
-    g = sh["gidx"][sel]
-    gpu = {"x": x[g], "y": y[g], "t": t[g], "p": p[g]}
-    gpu.update({c: out[c].cpu().numpy()[sel] for c in farms.COLUMNS[4:]})
-    rep = compare(gpu, {c: np.asarray(ref[c])[g] for c in farms.COLUMNS})
-    return {"events_compared": int(sel.size), "stream_prefix": k, "valid_events": rep["valid_ref"],
-            "valid_mismatch": rep["valid_mismatch"], "max_dtheta_true_rad": rep["theta_true_max_abs"],
-            "max_rel_r_true": rep["r_true_max_rel"], "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"],
-            "what": "rank 0's owned records of the stream's first K events vs the oracle on that prefix"}
 
 
 def host_path(fm, x, y, t, p, steps: int) -> dict:
@@ -237,54 +223,60 @@ def host_path(fm, x, y, t, p, steps: int) -> dict:
                     "overlapped per pooling super-chunk, copy-out and x/y/t/p echo (FARMS_HOST_THREADS threads)"}
 
 
-def rank_share(args, cfg: int, world: int, rank: int) -> dict:
-    """This rank's events of the weak-scaling stream (world x per-GPU events on
-    one sensor), generated without materialising the whole stream on any rank
-    (farms.synth_select): relative stamps (the stream's t0), clamped polarity."""
-    W, H = SENSOR[cfg]
-    fs = FILTER[cfg]
-    maxw = 50
+def stream_params(cfg: int, per_gpu: int, world: int):
     sp = farms.synth_params(cfg)
-    per_gpu = args.events or (int(sp.n_events) if cfg in (1, 2, 3) else 50_000_000)
-    n = per_gpu * world
-    sp.n_events = n
-    sh = {"per_gpu": per_gpu, "n_stream": n, "region": None, "owned": None, "seg": None, "cpu_sample": None,
-          "gidx": None}
-    if world == 1:
-        ev = farms.synth_generate(sp)
-        sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative()
-        if not args.no_cpu_baseline and not args.plan_only:
-            sh["cpu_sample"] = ev.head(min(args.cpu_sample, len(ev)))
-        sh.update(split="none", n_owned=n, label="1 GPU")
-    elif args.split == "segments":
-        lo, hi = segments.rank_window(n, world, rank)
-        ev, _, t_first = farms.synth_select(sp, lo, hi)
-        x, y, t, p = ev.relative(t_first)
-        seg, n_head = segments.plan_rank(t, lo, n, world, rank)  # raises on an unordered stream
-        sl = slice(seg.warm - lo, seg.end - lo)
-        sh["x"], sh["y"], sh["t"], sh["p"] = x[sl], y[sl], t[sl], p[sl]
-        sh["gidx"] = np.arange(seg.warm, seg.end, dtype=np.int64)
-        sh.update(split="segments", seg=seg, n_head=n_head, n_owned=seg.end - seg.start,
-                  label=(f"{world} temporal segments of the time-ordered stream: per step the ranks' last-stamp "
-                         f"surfaces are all-gathered and each rank starts from the merged SAE plus a re-fitted "
-                         f"500 us warm-up ({seg.n_warm} events on rank {rank})"))
-    else:
-        exch = args.split == "strips"
-        plan = strips.plan_hist(farms.synth_column_hist(sp), H, world, fs, maxw, exchange=exch)
-        strip = plan[rank]
-        ev, gidx, t_first = farms.synth_select(sp, 0, n, strip.reg_lo, strip.reg_hi)
-        sh["x"], sh["y"], sh["t"], sh["p"] = ev.relative(t_first)
-        sh["gidx"] = gidx
-        hl, hr = strips.halo(fs, maxw, W, H, exchange=exch)
-        sh.update(split=args.split, region=(strip.reg_lo, strip.reg_hi), owned=(strip.own_lo, strip.own_hi),
-                  n_owned=int(strips.owned_mask(sh["x"], strip).sum()))
-        if exch:
-            sh["lists"] = strips.exchange_lists(sh["x"], plan, rank)
-            sh["label"] = (f"{world} x-strips: each rank fits its owned columns and, per step, sends the local flows "
-                           f"of its events in other ranks' halos ({hl} / {hr} columns) with one grouped send/recv")
-        else:
-            sh["label"] = f"{world} x-strips, halos of {hl} / {hr} columns recomputed, no data-path collective"
-    return sh
+    sp.n_events = per_gpu * world
+    return sp
+
+
+def parity_multi(args, cfg, world, rank, dist, device, xdev, fm_kw) -> dict | None:
+    """N > 1: the same split and exchange as the timed steps, on a short stream
+    of N x parity_per_rank events of the same configuration (a share per rank),
+    run once; every rank's owned records are merged by stream index and rank 0
+    checks them against the oracle over the whole short stream — the bar of
+    tests/parity.py against the glibc oracle, every column bitwise against the
+    oracle with the GPU's correctly rounded libm — overall and per rank
+    boundary (multirank.boundary_events: each segment's first 500 us, each
+    strip border's pooling reach).  Returns rank 0's block (None elsewhere)."""
+    W, H = SENSOR[cfg]
+    jump, maxw = scales(cfg)
+    sp = stream_params(cfg, args.parity_per_rank, world)
+    hist = multirank.column_hist(sp, dist, rank, xdev) if args.split != "segments" else None
+    sh = multirank.make_share(sp, args.split, world, rank, FILTER[cfg], maxw, hist)
+    with farms.FlowManager(H, W, FILTER[cfg], 5, window_jump=jump, max_window=maxw, device=device.index,
+                           **fm_kw, **multirank.engine_args(sh)) as fm:
+        st = multirank.Stepper(fm, sh, dist, device, xdev)
+        dist.barrier()
+        st.step()
+        rec = st.owned_records()
+    merged = multirank.gather_owned(dist, rec, sh.n_stream)
+    if rank != 0:
+        return None
+    if merged is None:
+        return {"ok": False, "what": "the ranks' owned events do not partition the stream"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import OracleFlow
+    from parity import multi_report
+
+    ev = farms.synth_generate(sp)
+    x, y, t, p = ev.relative()
+    refs = {}
+
+    def run(libm):  # the two oracles in parallel threads (ctypes releases the GIL)
+        refs[libm] = OracleFlow(H, W, FILTER[cfg], 5, jump, maxw, libm=libm).process(x, y, t, p)
+
+    th = [threading.Thread(target=run, args=(m,)) for m in ("glibc", "cr")]
+    for a in th:
+        a.start()
+    for a in th:
+        a.join()
+    bnd = multirank.boundary_events(multirank.plan_info(sh), x, t, maxw, W, H)
+    rep = multi_report(merged, refs["glibc"], refs["cr"], bnd, maxw)
+    rep["what"] = (f"{world} ranks, split {args.split}, on a {sh.n_stream}-event stream of config {cfg}: every "
+                   f"rank's owned records vs the oracle over the whole stream (glibc: the tolerance bar; the "
+                   f"correctly rounded libm: bitwise), and per rank boundary")
+    return rep
 
 
 def main():
@@ -301,123 +293,76 @@ def main():
 
     # FARMS_BENCH_DEVICE pins every rank to one device (rehearsal of N ranks on a
     # one-GPU box, with FARMS_DIST_BACKEND=gloo); the driver uses neither.
-    device = int(os.environ.get("FARMS_BENCH_DEVICE", local_rank))
+    dev_idx = int(os.environ.get("FARMS_BENCH_DEVICE", local_rank))
     backend = os.environ.get("FARMS_DIST_BACKEND", "gloo" if args.plan_only else "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         if not args.plan_only:
-            torch.cuda.set_device(device)
+            torch.cuda.set_device(dev_idx)
         dist.init_process_group(backend)
-    red_dev = torch.device("cuda", device) if backend == "nccl" else torch.device("cpu")
+    device = torch.device("cuda", dev_idx)
+    xdev = device if backend == "nccl" else torch.device("cpu")  # where collectives run
 
     cfg = args.config
     W, H = SENSOR[cfg]
     fs = FILTER[cfg]
-    jump, maxw = (25, 50) if cfg == 5 else (5, 50)
-    sh = rank_share(args, cfg, world, rank)
-    x, y, t, p = sh["x"], sh["y"], sh["t"], sh["p"]
-    per_gpu, n_owned, split, seg, label = sh["per_gpu"], sh["n_owned"], sh["split"], sh["seg"], sh["label"]
-    cpu_sample = sh["cpu_sample"]
-    n = len(x)
+    jump, maxw = scales(cfg)
+    sp0 = farms.synth_params(cfg)
+    per_gpu = args.events or PER_GPU.get(cfg, int(sp0.n_events))
+    sp = stream_params(cfg, per_gpu, world)
+    hist = multirank.column_hist(sp, dist, rank, xdev if not args.plan_only else None) \
+        if world > 1 and args.split != "segments" else None
+    sh = multirank.make_share(sp, args.split, world, rank, fs, maxw, hist)
+    n, n_owned = sh.n, sh.n_owned
     if args.plan_only:
         total = n_owned
         if dist:
             tt = torch.tensor([n_owned], dtype=torch.int64)
             dist.all_reduce(tt)
             total = int(tt.item())
-        line = {"metric": "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref",
-                "value": None, "unit": "Mevents/s", "n_gpus": world, "plan_only": True,
-                "config": {"workload": f"BASELINE config {cfg}", "events_per_gpu": per_gpu, "parallelism": label},
-                "detail": {"owned_events_all_ranks": total, "stream_events": sh["n_stream"],
+        line = {"metric": METRIC, "value": None, "unit": "Mevents/s", "n_gpus": world, "plan_only": True,
+                "config": {"workload": f"BASELINE config {cfg}", "events_per_gpu": per_gpu, "parallelism": sh.label},
+                "detail": {"owned_events_all_ranks": total, "stream_events": sh.n_stream,
                            "rank0_stored_events": n, "rank0_owned_events": n_owned}}
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist:
             dist.destroy_process_group()
         return
-    dev = torch.device("cuda", device)
-    dx = torch.from_numpy(x).to(dev)
-    dy = torch.from_numpy(y).to(dev)
-    dt_ = torch.from_numpy(t.view(np.int32)).to(dev)
-    dp = torch.from_numpy(p).to(dev)
-    out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
-           for c in farms.COLUMNS[4:]}
-    lists = sh.get("lists")
-    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=device,
-                           fit_chunk=args.fit_chunk, pool_chunk=args.pool_chunk, pool_batch=args.pool_batch,
-                           region=sh["region"], owned=sh["owned"], import_halo=lists is not None)
-    if lists is not None:  # flow-halo exchange buffers, per peer
-        xdev = dev if backend == "nccl" else torch.device("cpu")
-        send_idx = {q: torch.from_numpy(a).to(dev) for q, (a, _) in lists.items()}
-        recv_idx = {q: torch.from_numpy(b).to(dev) for q, (_, b) in lists.items()}
-        send_buf = {q: torch.empty((len(a), 3), dtype=torch.float64, device=dev) for q, (a, _) in lists.items()}
-        recv_buf = {q: torch.empty((len(b), 3), dtype=torch.float64, device=dev) for q, (_, b) in lists.items()}
-        send_x = send_buf if xdev == dev else {q: v.cpu() for q, v in send_buf.items()}
-        recv_x = recv_buf if xdev == dev else {q: v.cpu() for q, v in recv_buf.items()}
-        n_halo_flows = sum(len(b) for _, b in lists.values())
-    if seg is not None:  # stamp surfaces: this rank's [head, full], everyone's, the merged SAE
-        n_head = sh["n_head"]
-        WHs = W * H
-        mine = torch.empty((2, WHs), dtype=torch.int64, device=dev)
-        gath = torch.empty((2 * world, WHs), dtype=torch.int64, device=red_dev)
-        rows = torch.tensor(segments.merge_rows(rank), dtype=torch.int64, device=dev)
-        sel = torch.empty((len(segments.merge_rows(rank)), WHs), dtype=torch.int64, device=dev)
-        sae = torch.empty(WHs, dtype=torch.int64, device=dev)
-        o = seg.n_warm  # the segment's own events start after the warm-up
+    fm_kw = {"fit_chunk": args.fit_chunk, "pool_chunk": args.pool_chunk, "pool_batch": args.pool_batch}
+    parity = None
+    if world > 1 and args.parity_per_rank > 0:
+        parity = parity_multi(args, cfg, world, rank, dist, device, xdev, fm_kw)
+    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, device=dev_idx, **fm_kw,
+                           **multirank.engine_args(sh))
+    st = multirank.Stepper(fm, sh, dist, device, xdev)
     torch.cuda.synchronize()
 
-    def step():
-        fm.reset()
-        if lists is not None:
-            fm.fit_device(dx, dy, dt_, dp, out)
-            for q in lists:
-                fm.export_flows(send_idx[q], send_buf[q])
-                if send_x[q] is not send_buf[q]:
-                    send_x[q].copy_(send_buf[q])
-            strips.exchange(dist, lists, send_x, recv_x)
-            torch.cuda.synchronize()
-            for q in lists:
-                if recv_x[q] is not recv_buf[q]:
-                    recv_buf[q].copy_(recv_x[q])
-                fm.import_flows(recv_idx[q], recv_buf[q])
-            fm.pool_device()
-            return
-        if seg is not None:
-            fm.last_stamps(dx[o:], dy[o:], dt_[o:], n_head, mine[0], mine[1])
-            dist.all_gather_into_tensor(gath, mine if red_dev == dev else mine.cpu())
-            if rank > 0:
-                torch.index_select(gath.to(dev, non_blocking=False), 0, rows, out=sel)
-                torch.cuda.synchronize()
-                fm.merge_stamps(sel, sae)
-                fm.seed_sae(sae)
-        fm.process_device(dx, dy, dt_, dp, out)
-
-    # HIP events around the k_pool launches (and phases) only; set before the
-    # warmup so that the timed steps replay the launch graph the warmup captured
+    # HIP events around the k_pool launches (and phases) only
     fm.set_profiling(farms.PROF_POOL)
     if dist:
         dist.barrier()  # communicators up on every rank before the first exchange
     for _ in range(args.warmup):
-        step()
+        st.step()
     stats = []
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        st.step()
         stats.append(fm.stats())
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=xdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        nn = torch.tensor([n_owned], device=red_dev, dtype=torch.float64)
+        nn = torch.tensor([n_owned], device=xdev, dtype=torch.float64)
         dist.all_reduce(nn)
         total_events = float(nn.item())
     else:
@@ -430,46 +375,41 @@ def main():
     pool_launches = ts["pool_launches"]
     # work counters (U_pool, candidates, contributors) from one more, untimed step
     fm.set_profiling(True)
-    step()
-    st = fm.stats()
+    st.step()
+    cs = fm.stats()
     avg_us = pool_ms * 1e3 / max(pool_launches, 1)
-    dense_bytes = 20.0 * st["pool_cells"]  # 20 B per dense pooling-window cell of a valid event
+    dense_bytes = 20.0 * cs["pool_cells"]  # 20 B per dense pooling-window cell of a valid event
     roofline = pool_roofline(cfg, world, pool_launches, avg_us, dense_bytes)
     line = {
-        "metric": "Mevents/s (and % HBM roofline) at 1/2/4/8 GPUs; max |dtheta| vs CPU ref",
-        "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC, "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"BASELINE config {cfg}: {W}x{H} synthetic moving-bars stream, "
                                f"{per_gpu} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
                    "events_per_gpu": per_gpu, "width": W, "height": H, "filtersize": fs,
-                   "parallelism": label},
+                   "parallelism": sh.label},
         "roofline": roofline,
-        "detail": {"valid_frac": round(st["n_valid"] / max(st["n_events"], 1), 4),
+        "detail": {"valid_frac": round(cs["n_valid"] / max(cs["n_events"], 1), 4),
                    "ms_prep": round(ts["ms_prep"], 3), "ms_fit_sweep": round(ts["ms_fit"], 3),
                    "ms_pool_sweep": round(ts["ms_pool"], 3), "ms_pool_kernel": round(pool_ms, 3),
-                   "ms_fit_kernel_untimed_step": round(st["ms_fit_kernel"], 3),
+                   "ms_fit_kernel_untimed_step": round(cs["ms_fit_kernel"], 3),
                    "dense_equiv_bytes_per_event": round(dense_bytes / max(n, 1), 1),
-                   "cand_per_valid": round(st["pool_candidates"] / max(st["n_valid"], 1), 1),
-                   "contrib_per_valid": round(st["pool_contributors"] / max(st["n_valid"], 1), 1)},
+                   "cand_per_valid": round(cs["pool_candidates"] / max(cs["n_valid"], 1), 1),
+                   "contrib_per_valid": round(cs["pool_contributors"] / max(cs["n_valid"], 1), 1)},
     }
     if world == 1 and args.host_steps > 0:
-        line["host_path"] = host_path(fm, x, y, t, p, args.host_steps)
+        line["host_path"] = host_path(fm, sh.x, sh.y, sh.t, sh.p, args.host_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ref, line["cpu_baseline"] = cpu_baseline(cpu_sample, W, H, fs, jump, maxw)
-        line["parity"] = parity_vs_cpu(ref, out, len(cpu_sample))
-    if world > 1 and rank == 0 and args.parity_sample > 0:
-        if seg is not None:
-            mask = np.zeros(n, bool)
-            mask[seg.n_warm:] = True
-        else:
-            mask = (x >= sh["owned"][0]) & (x < sh["owned"][1])
-        line["parity"] = parity_multi(args, cfg, sh, out, mask)
+        k = min(args.cpu_sample, n)
+        ref, line["cpu_baseline"] = cpu_baseline(sh.x, sh.y, sh.t, sh.p, k, W, H, fs, jump, maxw)
+        line["parity"] = parity_vs_cpu(ref, st.out, k)
+    if parity is not None:
+        line["parity"] = parity
     if world > 1:
         line["detail"]["rank0_stored_events"] = n
         line["detail"]["rank0_owned_events"] = n_owned
-        if lists is not None:
-            line["detail"]["rank0_halo_flows_received"] = n_halo_flows
+        if sh.lists is not None:
+            line["detail"]["rank0_halo_flows_received"] = st.n_halo_flows
     fm.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -64,6 +64,15 @@ def test_bad_parameters_are_rejected_before_touching_a_device():
     assert lib.farms_create(ctypes.byref(prm), ctypes.byref(h)) == farms.FARMS_EINVAL
     prm.window_jump, prm.max_window, prm.width = 5, 50, 0
     assert lib.farms_create(ctypes.byref(prm), ctypes.byref(h)) == farms.FARMS_EINVAL
+    # a stored region narrower than the owned columns' halo (vFlow.cpp:870-883,
+    # 1000): owned [100, 200) of a 1280 x 720 sensor needs [50, 251) with the
+    # flow exchange, [48, 253) when halo events are re-fitted (fs 5)
+    prm.width, prm.height, prm.filter_size = 1280, 720, 5
+    prm.own_x0, prm.own_x1 = 100, 200
+    for imp, lo, hi in [(1, 51, 251), (1, 50, 250), (0, 50, 251), (0, 48, 252)]:
+        prm.import_halo, prm.region_x0, prm.region_width = imp, lo, hi - lo
+        assert lib.farms_create(ctypes.byref(prm), ctypes.byref(h)) == farms.FARMS_EINVAL, (imp, lo, hi)
+        assert b"halo" in lib.farms_last_error()
 
 
 @pytest.mark.parametrize("cfg,W,H", [(1, 128, 128), (2, 320, 320), (3, 1280, 720)])

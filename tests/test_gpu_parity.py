@@ -63,6 +63,31 @@ def test_configs_vs_oracle(cfg, n, fs):
     assert rep["valid_ref"] > n // 20  # the stream really exercises pooling
 
 
+def test_config2_full_stream_vs_oracle():
+    """BASELINE config 2 at its full size (2M events, 320 x 320, fs 5): every
+    record against the oracle (both libms, run in parallel threads: ~40 s
+    each)."""
+    import threading
+
+    ev = farms.synth_config(2)
+    assert len(ev) == 2_000_000
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(320, 320, 5, 5) as fm:
+        g = fm.process(x, y, t, p)
+    refs = {}
+
+    def run(libm):
+        refs[libm] = OracleFlow(320, 320, 5, 5, libm=libm).process(x, y, t, p)
+
+    th = [threading.Thread(target=run, args=(m,)) for m in ("glibc", "cr")]
+    for a in th:
+        a.start()
+    for a in th:
+        a.join()
+    rep = assert_parity(g, refs["glibc"], 320, 320, rc=refs["cr"])
+    assert rep["valid_ref"] > 2_000_000 // 5
+
+
 def test_config4_stream_vs_oracle():
     """BASELINE config 4's own stream (seed 0x5EED0004, fs 7, 11 scales)."""
     ev = farms.synth_config(4, 150_000)
@@ -359,3 +384,23 @@ def test_serial_first_line_stamp_and_streaming():
     g2, _, _ = run_serial(first, x, y, t, p, 128, 128, 3, splits=[(0, 7), (7, 20_000), (20_000, len(x))],
                           fit_chunk=1000, pool_chunk=256)
     assert bitwise_equal(g, g2)
+
+
+def test_serial_first_only_on_a_fresh_handle():
+    """farms_serial_first after events would overwrite the previous-stamp source
+    of the serial pooling: refused until a reset.  The first line's stamp shows
+    in lastEventTime until an event fires at its pixel (vFlow.cpp:556)."""
+    with farms.FlowManager(32, 32, 3, 5, serial=True) as fm:
+        fm.serial_first(3, 4, 777)
+        lt = np.zeros(32 * 32)
+        fm._lib.farms_get_last_event_time(fm._h, lt.ctypes.data_as(__import__("ctypes").c_void_p))
+        assert lt[3 * 32 + 4] == 777
+        fm.process(np.array([1], np.int32), np.array([1], np.int32), np.array([5], np.uint32), np.array([1], np.int32))
+        with pytest.raises(farms.FarmsError) as ei:
+            fm.serial_first(3, 4, 777)
+        assert ei.value.code == farms.FARMS_EINVAL
+        fm.process(np.array([3], np.int32), np.array([4], np.int32), np.array([0], np.uint32), np.array([1], np.int32))
+        fm._lib.farms_get_last_event_time(fm._h, lt.ctypes.data_as(__import__("ctypes").c_void_p))
+        assert lt[3 * 32 + 4] == 0 and lt[1 * 32 + 1] == 5  # the event's own (relative) stamp 0 now
+        fm.reset()
+        fm.serial_first(3, 4, 777)

@@ -197,6 +197,45 @@ def test_engine_strips_are_bitwise_the_whole_run(n_strips, fs, exchange):
 
 
 @pytest.mark.gpu
+def test_import_halo_handle_guards():
+    """An import_halo handle refuses the one-phase calls (they would pool
+    without the halo flows), and halo flows that are never imported count as
+    invalid: the records do not depend on what the workspace held before."""
+    W, H, fs = 1280, 720, 5
+    ev = farms.synth_config(3, 200_000)
+    x, y, t, p = ev.relative()
+    plan = strips.plan(x, W, H, 3, fs, 50)
+    s = plan[1]
+    m = strips.region_mask(x, s)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x[m], y[m], t[m].view(np.int32), p[m])]
+    with farms.FlowManager(H, W, fs, 5, region=(s.reg_lo, s.reg_hi), owned=(s.own_lo, s.own_hi),
+                           import_halo=True) as fm:
+        with pytest.raises(farms.FarmsError) as ei:
+            fm.process(x[m], y[m], t[m], p[m])
+        assert ei.value.code == farms.FARMS_EINVAL
+        outs = []
+        for garbage in (False, True):
+            if garbage:  # dirty the workspace with a different stream first
+                fm.reset()
+                g = [torch.flip(a, [0]).contiguous() for a in d]
+                fm.fit_device(*g, {c: torch.zeros(len(g[0]), dtype=torch.int32 if c == "scale" else torch.float64,
+                                                  device=dev) for c in COLS[4:]})
+                fm.pool_device()
+            fm.reset()
+            o = {c: torch.zeros(int(m.sum()), dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+                 for c in COLS[4:]}
+            fm.fit_device(*d, o)
+            fm.pool_device()  # no import: every halo flow invalid
+            outs.append({c: o[c].cpu().numpy() for c in COLS[4:]})
+    own = strips.owned_mask(x[m], s)
+    for c in COLS[4:]:
+        a, b = outs[0][c][own], outs[1][c][own]
+        assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                              b.view(np.int64) if b.dtype == np.float64 else b), c
+
+
+@pytest.mark.gpu
 def test_engine_strips_narrow_and_short_sensors():
     """Strips narrower than the halo (flows from two ranks away) on a square
     sensor, and a sensor lower than maxWindow where the W-1 clip reaches two

@@ -185,6 +185,7 @@ struct Ctx {
     CandVal *val_ring;
     int64_t nwords;
     int NB, C2;            // ring size, events per pooling chunk
+    int ring0;             // ring buffer of the call's first pooling chunk (chunk numbers continue across calls)
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
@@ -1536,7 +1537,7 @@ __global__ __launch_bounds__(64, 4) void k_chain(Ctx c, int ch0, int ch1) {
     // wait for them here, once
     asm volatile("" ::"v"(tmin_l), "v"(tmax_l));
     for (int ch = ch0; ch < ch1; ++ch) {
-        const int b = ch % c.NB;
+        const int b = (c.ring0 + ch) % c.NB;
         const int ce = min((ch + 1) * C2, n);
         const uint32_t tmin = (uint32_t)__builtin_amdgcn_readlane((int)tmin_l, ch - ch0);
         const uint32_t tmax = (uint32_t)__builtin_amdgcn_readlane((int)tmax_l, ch - ch0);
@@ -2071,7 +2072,7 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     if (d.x < 0) return;  // invalid flow, or a halo event (pooled by its owner)
     const int e = d.x, ex = d.y, ey = d.z;
     const uint32_t teu = (uint32_t)d.w;
-    const int buf = (w / c.C2) % c.NB;  // the event's chunk's candidate buffer
+    const int buf = (c.ring0 + w / c.C2) % c.NB;  // the event's chunk's candidate buffer
     pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
 }
 
@@ -2210,6 +2211,34 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // ===========================================================================
 // handle
 
+// Per-call workspace.  Two sets: the host-array path pipelines a call in
+// sub-batches, and sub-batch b + 1's upload and prep (set (b+1) % 2) run while
+// sub-batch b's sweeps still read set b % 2.
+struct Work {
+    int64_t cap = 0;
+    int32_t *x = nullptr, *y = nullptr, *p = nullptr;  // device copies of host inputs (farms_process)
+    uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
+    int32_t *iota = nullptr, *P = nullptr;
+    int2 *PT = nullptr;
+    int4 *link = nullptr;
+    int32_t *Q = nullptr;
+    int4 *qe = nullptr;
+    double2 *plane = nullptr;
+    uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
+    uint8_t *valid = nullptr;
+    FlowCell *evf = nullptr;
+    int2 *dbg_tc = nullptr;
+    double *o_d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // records (farms_process)
+    int32_t *o_scale = nullptr;
+    uint32_t *ctmin = nullptr, *ctmax = nullptr;
+    void *cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
+    std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
+    hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
+    bool busy = false;                         // `done` recorded and the set not yet reused
+};
+
 struct farms_handle {
     farms_params prm;
     int W = 0, H = 0, fr = 0, J = 0, M = 0, K = 0;
@@ -2219,11 +2248,10 @@ struct farms_handle {
     hipStream_t stream = nullptr;
     // persistent surfaces (x-major, W*H cells)
     SaeCell *cells = nullptr;
-    int2 *PT = nullptr;
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    int32_t *pcur = nullptr, *pend = nullptr;
-    // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1)
+    // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1), indexed by
+    // the chunk's number since the last reset (calls continue the ring)
     int pool_batch = kDefaultPoolBatch, NB = 2 * kDefaultPoolBatch + 1;
     BmWord *bw_ring = nullptr;
     int nblk = 0;
@@ -2231,18 +2259,12 @@ struct farms_handle {
     CandHdr *hdr_ring = nullptr;
     CandVal *val_ring = nullptr;
     int64_t nwords = 0;
+    int64_t chunk_base = 0, super_base = 0;  // pooling chunks / super-chunks enqueued since the last reset
+    hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
+    hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
     hipStream_t s_chain = nullptr, s_pool = nullptr;  // candidate-building chain, pooling kernels
-    std::vector<hipEvent_t> sync_ev;                  // dependency events (no timing)
     uint32_t seq = 0;
-    // per-call workspace
-    int64_t cap = 0;
-    int32_t *x = nullptr, *y = nullptr, *p = nullptr;
-    uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
-    int32_t *iota = nullptr, *P = nullptr;
-    int4 *link = nullptr;
-    int32_t *Q = nullptr;
-    int4 *qe = nullptr;
-    double2 *plane = nullptr;
+    Work ws[2];
     // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
     const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
     const uint32_t *ph_t = nullptr;
@@ -2251,17 +2273,8 @@ struct farms_handle {
     int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
     uint32_t first_t = 0;
     bool fresh = true;          // no event since create / reset (farms_serial_first's precondition)
-    uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     int tile_bits = 0;
-    int tile_shift = 3;       // work-order tile: 2^tile_shift square (FARMS_POOL_TILE)
-    uint8_t *valid = nullptr;
-    FlowCell *evf = nullptr;
-    int2 *dbg_tc = nullptr;
-    double *o_d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    int32_t *o_scale = nullptr;
-    uint32_t *ctmin = nullptr, *ctmax = nullptr;
-    void *cub_tmp = nullptr;
-    size_t cub_bytes = 0;
+    int tile_shift = 3;       // work-order tile: 2^tile_shift square
     int *err = nullptr;
     unsigned long long *counters = nullptr;
     bool profiling = false;  // kernel timing events
@@ -2271,12 +2284,14 @@ struct farms_handle {
     std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
     farms_stats stats{};
     // host-array path (farms_process): pinned staging of inputs (16 B/event)
-    // and records (52 B/event), a copy stream for the record downloads, one
-    // completion event per pooling super-chunk
+    // and records (52 B/event, or 68 with the x/y/t/p echo), an upload and a
+    // download stream, one completion event per pooling super-chunk, one per
+    // sub-batch upload
     uint8_t *pin_in = nullptr, *pin_out = nullptr;
     int64_t pin_cap = 0;
-    hipStream_t s_copy = nullptr;
+    hipStream_t s_copy = nullptr, s_up = nullptr;
     std::vector<hipEvent_t> copy_ev;
+    hipEvent_t up_ev[2] = {};
 };
 
 namespace {
@@ -2293,15 +2308,15 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
-void free_workspace(farms_handle *h) {
-    dfree(h->x); dfree(h->y); dfree(h->p); dfree(h->t); dfree(h->pix); dfree(h->skey);
-    dfree(h->iota); dfree(h->P); dfree(h->PT); dfree(h->link);
-    dfree(h->Q); dfree(h->qe); dfree(h->plane); dfree(h->wkey); dfree(h->wkey_sorted);
-    dfree(h->valid); dfree(h->evf); dfree(h->dbg_tc); dfree(h->o_scale); dfree(h->ctmin); dfree(h->ctmax);
-    for (auto &d : h->o_d) dfree(d);
-    dfree(h->cub_tmp);
-    h->cub_bytes = 0;
-    h->cap = 0;
+void free_workspace(Work &w) {
+    dfree(w.x); dfree(w.y); dfree(w.p); dfree(w.t); dfree(w.pix); dfree(w.skey);
+    dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
+    dfree(w.Q); dfree(w.qe); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
+    dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.o_scale); dfree(w.ctmin); dfree(w.ctmax);
+    for (auto &d : w.o_d) dfree(d);
+    dfree(w.cub_tmp);
+    w.cub_bytes = 0;
+    w.cap = 0;
 }
 
 int end_bit_for(int64_t WH) {
@@ -2310,46 +2325,59 @@ int end_bit_for(int64_t WH) {
     return b;
 }
 
-int ensure_capacity(farms_handle *h, int64_t n) {
-    if (n <= h->cap) return FARMS_OK;
-    free_workspace(h);
+// Every stream of the handle idle (nothing of an asynchronous call in flight).
+int sync_all(farms_handle *h) {
+    for (hipStream_t s : {h->stream, h->s_chain, h->s_pool, h->s_copy, h->s_up})
+        if (s) HIPCHK(hipStreamSynchronize(s));
+    for (Work &w : h->ws) w.busy = false;
+    return FARMS_OK;
+}
+
+int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
+    if (n <= w.cap) return FARMS_OK;
+    int rc = sync_all(h);  // the set may still be read by an earlier call
+    if (rc) return rc;
+    free_workspace(w);
     const int64_t cap = n;
     const int64_t nch = (cap + h->pool_chunk - 1) / h->pool_chunk;
-    int rc;
-    if ((rc = dalloc(&h->x, cap)) || (rc = dalloc(&h->y, cap)) || (rc = dalloc(&h->p, cap)) ||
-        (rc = dalloc(&h->t, cap)) || (rc = dalloc(&h->pix, cap)) || (rc = dalloc(&h->skey, cap)) ||
-        (rc = dalloc(&h->iota, cap)) || (rc = dalloc(&h->P, cap)) || (rc = dalloc(&h->PT, cap)) || (rc = dalloc(&h->link, cap)) ||
-        (rc = dalloc(&h->Q, cap)) || (rc = dalloc(&h->qe, cap)) || (rc = dalloc(&h->plane, cap)) || (rc = dalloc(&h->wkey, cap)) || (rc = dalloc(&h->wkey_sorted, cap)) ||
-        (rc = dalloc(&h->valid, cap)) ||
-        (rc = dalloc(&h->evf, cap)) || (rc = dalloc(&h->dbg_tc, cap)) ||
-        (rc = dalloc(&h->o_scale, cap)) || (rc = dalloc(&h->ctmin, nch)) ||
-        (rc = dalloc(&h->ctmax, nch))) {
-        free_workspace(h);
+    if ((rc = dalloc(&w.x, cap)) || (rc = dalloc(&w.y, cap)) || (rc = dalloc(&w.p, cap)) ||
+        (rc = dalloc(&w.t, cap)) || (rc = dalloc(&w.pix, cap)) || (rc = dalloc(&w.skey, cap)) ||
+        (rc = dalloc(&w.iota, cap)) || (rc = dalloc(&w.P, cap)) || (rc = dalloc(&w.PT, cap)) ||
+        (rc = dalloc(&w.link, cap)) || (rc = dalloc(&w.Q, cap)) || (rc = dalloc(&w.qe, cap)) ||
+        (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
+        (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
+        (rc = dalloc(&w.o_scale, cap)) || (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch))) {
+        free_workspace(w);
         return rc;
     }
-    for (auto &d : h->o_d)
-        if ((rc = dalloc(&d, cap))) { free_workspace(h); return rc; }
+    for (auto &d : w.o_d)
+        if ((rc = dalloc(&d, cap))) { free_workspace(w); return rc; }
     size_t bytes = 0, bytes2 = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, h->pix, h->skey, h->iota, h->P, (int)cap, 0,
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, w.pix, w.skey, w.iota, w.P, (int)cap, 0,
                                               end_bit_for(h->WH), h->stream));
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, h->wkey, h->wkey_sorted, h->iota, h->Q, (int)cap, 0,
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, w.wkey, w.wkey_sorted, w.iota, w.Q, (int)cap, 0,
                                               32, h->stream));
     bytes = std::max(bytes, bytes2);
-    if ((rc = dalloc((uint8_t **)&h->cub_tmp, bytes))) { free_workspace(h); return rc; }
-    h->cub_bytes = bytes;
-    h->cap = cap;
+    if ((rc = dalloc((uint8_t **)&w.cub_tmp, bytes))) { free_workspace(w); return rc; }
+    w.cub_bytes = bytes;
+    w.cap = cap;
     return FARMS_OK;
 }
 
 int reset_surfaces(farms_handle *h) {
+    int rc = sync_all(h);
+    if (rc) return rc;
     // tag 0: never visited, never touched (chunk seqs start at 1)
     HIPCHK(hipMemsetAsync(h->cells, 0, 2 * sizeof(SaeCell) * h->WH, h->stream));  // both SAE buffers
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->pcur, 0, sizeof(int32_t) * h->WH, h->stream));
-    HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
+    for (Work &w : h->ws) {
+        HIPCHK(hipMemsetAsync(w.pcur, 0, sizeof(int32_t) * h->WH, h->stream));
+        HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
+    h->chunk_base = h->super_base = 0;
     h->first_q = -1;
     h->fresh = true;
     return FARMS_OK;
@@ -2421,25 +2449,32 @@ int ensure_kernel_events(farms_handle *h, size_t count) {
     return FARMS_OK;
 }
 
-int ensure_sync_events(farms_handle *h, size_t count) {
-    while (h->sync_ev.size() < count) {
+int ensure_sync_events(Work &w, size_t count) {
+    while (w.sync_ev.size() < count) {
         hipEvent_t ev;
         HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        h->sync_ev.push_back(ev);
+        w.sync_ev.push_back(ev);
     }
     return FARMS_OK;
 }
 
-// The whole per-event loop for n device-resident events.  on_super (may be
-// null) is called as soon as the work of pooling super-chunk S (events [p0,
-// p1)) is enqueued, with the event that marks its records final on the device:
-// the host-array path starts the download of those records there.
-// phase 0 runs the whole loop; phase 1 only prep and the local fits (then
-// synchronizes), phase 2 only the pooling sweep of the events phase 1 saw: the
-// x-strip exchange of halo flows (farms_import_flows) goes between the two.
+// The whole per-event loop for n device-resident events, with workspace set w.
+// on_super (may be null) is called as soon as the work of pooling super-chunk
+// S (events [p0, p1)) is enqueued, with the event that marks its records final
+// on the device: the host-array path starts the download of those records
+// there.  phase 0 runs the whole loop; phase 1 only prep and the local fits
+// (then synchronizes), phase 2 only the pooling sweep of the events phase 1
+// saw: the x-strip exchange of halo flows (farms_import_flows) goes between
+// the two.
+// Asynchronous calls (phase 0, `async`; the host-array path's sub-batches)
+// return once everything is enqueued: every stream's work of the call is
+// ordered before w.done, consecutive calls chain on the streams (F: SAE, C:
+// flow snapshots and cursors, P), the candidate ring continues by chunk number,
+// and `validated` skips the device-side range check (and its host sync).
 typedef std::function<int(int S, int p0, int p1, hipEvent_t done)> super_hook;
-int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
-             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0) {
+int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
+             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0,
+             bool async = false, bool validated = false) {
     const int n = (int)n64;
     hipStream_t s = h->stream;
     h->fresh = false;
@@ -2452,15 +2487,16 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
-    c.pix = h->pix; c.skey = h->skey; c.P = h->P; c.link = h->link;
-    c.Q = h->Q; c.qe = h->qe; c.plane = h->plane;
-    c.cells = h->cells; c.PT = h->PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
-    c.evf = h->evf; c.valid = h->valid; c.ctmin = h->ctmin; c.ctmax = h->ctmax;
-    c.pcur = h->pcur; c.pend = h->pend;
+    c.pix = w.pix; c.skey = w.skey; c.P = w.P; c.link = w.link;
+    c.Q = w.Q; c.qe = w.qe; c.plane = w.plane;
+    c.cells = h->cells; c.PT = w.PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
+    c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
+    c.pcur = w.pcur; c.pend = w.pend;
     c.serial = h->prm.serial != 0;
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
+    c.ring0 = (int)(h->chunk_base % h->NB);
     const int span = 2 * h->M + 1;  // pooling window rows and columns
     c.pool_bw = (span * span + 63) / 64 + 1;  // flattened window positions (+1: a two-half step reads a word ahead)
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
@@ -2469,12 +2505,16 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
     if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
     c.counters = h->counters;
-    c.dbg_tc = h->counting ? h->dbg_tc : nullptr;
+    c.dbg_tc = h->counting && !async ? w.dbg_tc : nullptr;
 
-    const bool prof = h->profiling;
+    const bool prof = h->profiling && !async;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
     const int B = h->pool_batch;
     const int n_super = ceil_div(n_pool_chunks, B);
+    if (w.busy) {  // the set's previous (asynchronous) call is done with it before anything writes it
+        HIPCHK(hipStreamWaitEvent(s, w.done, 0));
+        w.busy = false;
+    }
     if (prof) {
         int rc = ensure_kernel_events(h, 2 * (size_t)(n_fit_chunks + n_super));
         if (rc) return rc;
@@ -2483,40 +2523,45 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
     // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
     {
-        int rc = ensure_sync_events(h, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
+        int rc = ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
         if (rc) return rc;
     }
-    hipEvent_t ev_prep = h->sync_ev[0];
-    auto ev_fit = [&](int f) { return h->sync_ev[1 + f]; };
-    auto ev_cand = [&](int S) { return h->sync_ev[1 + n_fit_chunks + 2 * S]; };
-    auto ev_pool = [&](int S) { return h->sync_ev[2 + n_fit_chunks + 2 * S]; };
+    hipEvent_t ev_prep = w.sync_ev[0];
+    auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
+    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
+    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
 
     // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
     if (phase == 2) {  // prepared by phase 1
         if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
         HIPCHK(hipEventRecord(ev_prep, s));
     } else {
-    HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->pix, h->iota, h->wkey, h->err,
+    if (!validated) HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err,
                        h->pool_chunk, h->tile_bits, h->tile_shift);
-    int herr = 0;
-    HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (herr) return fail(FARMS_EINVAL, "event outside the width x height sensor");
-    size_t bytes = h->cub_bytes;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->pix, h->skey, h->iota, h->P, n, 0,
+    if (!validated) {
+        int herr = 0;
+        HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (herr) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+    }
+    size_t bytes = w.cub_bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, bytes, w.pix, w.skey, w.iota, w.P, n, 0,
                                               end_bit_for(h->WH), s));
-    HIPCHK(hipMemsetAsync(h->pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
-    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, h->link, h->PT, h->prm.serial != 0);
+    HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
+    // serial mode: k_link reads the flow snapshots' stamps, final once the
+    // previous call's chain is done
+    if (c.serial && h->super_base > 0) HIPCHK(hipStreamWaitEvent(s, h->chain_end, 0));
+    hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.link, w.PT, h->prm.serial != 0);
     {
         int cb = 1;
         while ((1 << cb) < n_pool_chunks) ++cb;
         if (cb + h->tile_bits > 32) return fail(FARMS_EINVAL, "too many pooling chunks for one call; raise pool_chunk");
-        size_t b2 = h->cub_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, b2, h->wkey, h->wkey_sorted, h->iota, h->Q, n, 0,
+        size_t b2 = w.cub_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, b2, w.wkey, w.wkey_sorted, w.iota, w.Q, n, 0,
                                                   h->tile_bits + cb, s));
     }
-    hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, h->ctmin, h->ctmax);
+    hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
     }  // prep
@@ -2526,7 +2571,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
     //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
     //     or k_fit_wave for filters without a compile-time fast path);
     //   stream C: the candidate chain, one k_chain per pooling chunk, each
-    //     chunk's records into ring buffer ch % NB (NB = 2B + 1);
+    //     chunk's records into ring buffer (chunk number) % NB (NB = 2B + 1);
     //   stream P: one k_pool per super-chunk of B pooling chunks.
     // Pooling of a chunk reads only its candidate buffer, the per-event flows
     // and P, so it overlaps the chain of later chunks and the fit sweep.
@@ -2570,7 +2615,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         if (fast_fit) {
             merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
-            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, h->Q + c0,
+            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, w.Q + c0,
                                c1 - c0);
         }
         if (!merged && next.blocks > 0) launch_prep(next);
@@ -2606,8 +2651,10 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         return FARMS_OK;
     }
     if (phase == 2) { fit_enqueued = n_fit_chunks; fit_waited = n_fit_chunks - 1; }  // fits done (phase 1)
+    const int64_t sb = h->super_base;  // global number of this call's first super-chunk
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
+        const int64_t Sg = sb + S;
         // keep the fit sweep one super-chunk ahead of the chain
         const int need = std::min(n_fit_chunks, ceil_div(std::min<int64_t>((int64_t)(ch1 + B) * h->pool_chunk, n),
                                                          h->fit_chunk));
@@ -2615,7 +2662,8 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
             int rc = enqueue_fit(fit_enqueued++);
             if (rc) return rc;
         }
-        if (S >= 2) HIPCHK(hipStreamWaitEvent(sc, ev_pool(S - 2), 0));  // ring buffers of S-2 are free
+        // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
+        if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
         {  // the chain reads the local flows of every event of the super-chunk
             const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
             const int fl = std::min(f, n_fit_chunks - 1);
@@ -2640,6 +2688,7 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
         hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
         HIPCHK(hipEventRecord(ev_pool(S), sp));
+        HIPCHK(hipEventRecord(h->gpool[Sg % 3], sp));
         if (on_super) {
             int rc = (*on_super)(S, p0, p1, ev_pool(S));
             if (rc) return rc;
@@ -2649,13 +2698,25 @@ int run_core(farms_handle *h, const int32_t *dx, const int32_t *dy, const uint32
         int rc = enqueue_fit(fit_enqueued++);
         if (rc) return rc;
     }
+    h->super_base += n_super;
+    h->chunk_base += n_pool_chunks;
+    if (n_super > 0) HIPCHK(hipEventRecord(h->chain_end, sc));
     HIPCHK(hipGetLastError());
     const int pool_launches = n_super;
-    HIPCHK(hipGetLastError());
     // join: stream F waits for the last chain step and the last pooling launch
     if (n_super > 0) {
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
+    }
+    if (async) {
+        HIPCHK(hipEventRecord(w.done, s));
+        w.busy = true;
+        farms_stats st{};
+        st.n_events = n;
+        st.fit_launches = fit_launches;
+        st.pool_launches = pool_launches;
+        h->stats = st;
+        return FARMS_OK;
     }
     if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
     if (h->counting) {
@@ -2812,8 +2873,17 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
+    {
+        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->up_ev[0],
+                                         &h->up_ev[1], &h->ws[0].done, &h->ws[1].done};
+        for (hipEvent_t *ev : evs)
+            if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
+                return bail(fail(FARMS_EHIP, "hipEventCreate"));
+    }
     if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->pcur, h->WH)) || (rc = dalloc(&h->pend, h->WH)) ||
+        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ws[0].pcur, h->WH)) ||
+        (rc = dalloc(&h->ws[0].pend, h->WH)) || (rc = dalloc(&h->ws[1].pcur, h->WH)) ||
+        (rc = dalloc(&h->ws[1].pend, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
         (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
@@ -2827,16 +2897,28 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
-    free_workspace(h);
+    if (h->s_copy) (void)hipStreamSynchronize(h->s_copy);
+    if (h->s_up) (void)hipStreamSynchronize(h->s_up);
     dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
-    dfree(h->pcur); dfree(h->pend); dfree(h->bw_ring);
+    for (Work &w : h->ws) {
+        free_workspace(w);
+        dfree(w.pcur); dfree(w.pend);
+        for (auto &ev : w.sync_ev) (void)hipEventDestroy(ev);
+        if (w.done) (void)hipEventDestroy(w.done);
+    }
+    for (auto &ev : h->gpool)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto &ev : h->up_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->chain_end) (void)hipEventDestroy(h->chain_end);
+    dfree(h->bw_ring);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);
-    for (auto &ev : h->sync_ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->copy_ev) (void)hipEventDestroy(ev);
-    if (h->s_copy) { (void)hipStreamSynchronize(h->s_copy); (void)hipStreamDestroy(h->s_copy); }
+    if (h->s_copy) (void)hipStreamDestroy(h->s_copy);
+    if (h->s_up) (void)hipStreamDestroy(h->s_up);
     if (h->pin_in) (void)hipHostFree(h->pin_in);
     if (h->pin_out) (void)hipHostFree(h->pin_out);
     if (h->s_pool) (void)hipStreamDestroy(h->s_pool);
@@ -2971,8 +3053,8 @@ extern "C" int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32
     h->ph_n = -1;
     if (n == 0) return FARMS_OK;
     HIPCHK(hipSetDevice(h->prm.device));
-    if ((rc = ensure_capacity(h, n))) return rc;
-    if ((rc = run_core(h, d_x, d_y, d_t, d_p, n, d_out, nullptr, 1))) return rc;
+    if ((rc = ensure_capacity(h, h->ws[0], n))) return rc;
+    if ((rc = run_core(h, h->ws[0], d_x, d_y, d_t, d_p, n, d_out, nullptr, 1))) return rc;
     h->ph_x = d_x; h->ph_y = d_y; h->ph_t = d_t; h->ph_p = d_p; h->ph_n = n; h->ph_out = *d_out;
     return FARMS_OK;
 }
@@ -2983,7 +3065,7 @@ extern "C" int farms_pool_device(farms_handle *h) {
     HIPCHK(hipSetDevice(h->prm.device));
     const int64_t n = h->ph_n;
     h->ph_n = -1;
-    return run_core(h, h->ph_x, h->ph_y, h->ph_t, h->ph_p, n, &h->ph_out, nullptr, 2);
+    return run_core(h, h->ws[0], h->ph_x, h->ph_y, h->ph_t, h->ph_p, n, &h->ph_out, nullptr, 2);
 }
 
 extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
@@ -2992,7 +3074,7 @@ extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t
     if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_export_flows outside a fit / pool pair");
     HIPCHK(hipSetDevice(h->prm.device));
     if (count > 0)
-        hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->evf, d_idx,
+        hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->ws[0].evf, d_idx,
                            (int)count, d_flows);
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
@@ -3005,7 +3087,7 @@ extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t
     if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_import_flows outside a fit / pool pair");
     HIPCHK(hipSetDevice(h->prm.device));
     Ctx c{};
-    c.t = h->ph_t; c.evf = h->evf; c.valid = h->valid;
+    c.t = h->ph_t; c.evf = h->ws[0].evf; c.valid = h->ws[0].valid;
     if (count > 0)
         hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, c, d_idx, (int)count,
                            d_flows);
@@ -3024,9 +3106,9 @@ extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const i
         !d_out->r_local || !d_out->theta_local || !d_out->scale)
         return fail(FARMS_EINVAL, "null array");
     HIPCHK(hipSetDevice(h->prm.device));
-    int rc = ensure_capacity(h, n);
+    int rc = ensure_capacity(h, h->ws[0], n);
     if (rc) return rc;
-    return run_core(h, d_x, d_y, d_t, d_p, n, d_out);
+    return run_core(h, h->ws[0], d_x, d_y, d_t, d_p, n, d_out);
 }
 
 namespace {
@@ -3050,17 +3132,49 @@ int ensure_pinned(farms_handle *h, int64_t n) {
     return FARMS_OK;
 }
 
+// Host memory the DMA engines reach directly (hipHostMalloc'd or registered):
+// such arrays skip the pinned staging copy.
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error here
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// fn(a, b) over [0, n) split into T slices on host threads (inline when one)
+template <class Fn>
+void host_parallel(int64_t n, int T, Fn &&fn) {
+    const int64_t slice = std::max<int64_t>((n + T - 1) / T, 1 << 16);
+    std::vector<std::thread> th;
+    for (int64_t a = 0; a < n; a += slice) {
+        const int64_t b = std::min(n, a + slice);
+        if (b == n && th.empty()) fn(a, b);
+        else th.emplace_back([=, &fn] { fn(a, b); });
+    }
+    for (auto &w : th) w.join();
+}
+
 }  // namespace
 
-// Host arrays in and out (the CLI path, vFlow.cpp:214-416 timed region).
-//   upload: host threads copy slices of x, y, t, p into pinned staging and each
-//     enqueues its slice's DMA right away (copies and DMA overlap);
-//   compute: run_core, unchanged;
-//   download: as each pooling super-chunk's records become final on the device
-//     (run_core's hook), its seven columns are DMAed into pinned staging on a
-//     copy stream while later super-chunks compute, and host threads move them
-//     into the caller's arrays (with the x, y, t, p echo) as each DMA lands.
-// Only the last super-chunk's download and copy-out are not hidden by compute.
+// Host arrays in and out (the CLI path, vFlow.cpp:214-416 timed region),
+// pipelined in sub-batches of whole pooling super-chunks (about an eighth of
+// a long call each; consecutive calls are bitwise one call):
+//   upload: sub-batch b's events are range-checked and (pageable arrays)
+//     copied into pinned staging by host threads, then DMAed on the upload
+//     stream into workspace set b % 2 -- while the GPU still computes
+//     sub-batch b - 1 (run_core enqueues asynchronously);
+//   compute: run_core on set b % 2, chained on the streams behind b - 1;
+//   download: as each pooling super-chunk's records become final on the
+//     device (run_core's hook) its columns are DMAed -- straight into the
+//     caller's arrays when they are pinned (with the x, y, t, p echo from the
+//     device copies), else into pinned staging, moved to the caller's arrays
+//     (with the echo) by host threads as each DMA lands.
+// Only the first sub-batch's upload and the last super-chunk's download are
+// not hidden by compute.  An event outside the sensor stops the call with
+// FARMS_EINVAL before its sub-batch is enqueued (earlier sub-batches of a long
+// call have then been processed: reset the handle to start over).
 extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
@@ -3071,70 +3185,68 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         !out->vx || !out->vy || !out->r_local || !out->theta_local || !out->scale)
         return fail(FARMS_EINVAL, "null array");
     HIPCHK(hipSetDevice(h->prm.device));
-    int rc = ensure_capacity(h, n);
-    if (rc) return rc;
-    if ((rc = ensure_pinned(h, n))) return rc;
-    if (!h->s_copy) HIPCHK(hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking));
-    hipStream_t s = h->stream;
-    const int T = host_threads();
-
-    // ---- upload: pinned layout x | y | t | p, n entries each
-    int32_t *px = reinterpret_cast<int32_t *>(h->pin_in), *py = px + n, *pp = py + n;
-    uint32_t *pt = reinterpret_cast<uint32_t *>(pp + n);
-    {
-        std::vector<std::thread> th;
-        std::atomic<int> bad{0};
-        const int64_t slice = std::max<int64_t>((n + T - 1) / T, 1 << 16);
-        for (int64_t a = 0; a < n; a += slice) {
-            const int64_t b = std::min(n, a + slice);
-            auto job = [=, &bad]() {
-                const size_t k = (size_t)(b - a);
-                std::memcpy(px + a, x + a, 4 * k);
-                std::memcpy(py + a, y + a, 4 * k);
-                std::memcpy(pt + a, t + a, 4 * k);
-                std::memcpy(pp + a, p + a, 4 * k);
-                if (hipMemcpyAsync(h->x + a, px + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(h->y + a, py + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(h->t + a, pt + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(h->p + a, pp + a, 4 * k, hipMemcpyHostToDevice, s) != hipSuccess)
-                    bad = 1;
-            };
-            if (b == n && th.empty()) job();  // one slice: no thread
-            else th.emplace_back(job);
-        }
-        for (auto &w : th) w.join();
-        if (bad) return fail(FARMS_EHIP, "farms_process: host-to-device copy");
+    // sub-batches of whole super-chunks, about n / 8 (at least 4 super-chunks);
+    // profiled or counted calls stay one call (their figures are per call)
+    const int64_t super = (int64_t)h->pool_chunk * h->pool_batch;
+    int64_t sub = n;
+    if (!h->profiling && !h->counting) {
+        const int64_t per = std::max<int64_t>(4 * super, (n / 8 + super - 1) / super * super);
+        if (n > 2 * per) sub = per;
     }
-
-    // ---- compute, with the record downloads hooked onto each super-chunk
-    farms_records d{};
-    d.r_true = h->o_d[0]; d.theta_true = h->o_d[1]; d.vx = h->o_d[2]; d.vy = h->o_d[3];
-    d.r_local = h->o_d[4]; d.theta_local = h->o_d[5]; d.scale = h->o_scale;
-    // pinned layout of the records: six double columns, then scale
-    double *pcol[6];
-    for (int k = 0; k < 6; ++k) pcol[k] = reinterpret_cast<double *>(h->pin_out) + (size_t)k * n;
-    int32_t *pscale = reinterpret_cast<int32_t *>(reinterpret_cast<double *>(h->pin_out) + 6 * (size_t)n);
-    double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
+    const int nbat = ceil_div(n, sub);
+    int rc = ensure_capacity(h, h->ws[0], sub);
+    if (!rc && nbat > 1) rc = ensure_capacity(h, h->ws[1], sub);
+    if (rc) return rc;
+    // per array: pinned host memory is DMAed directly, pageable memory goes
+    // through the handle's pinned staging
+    const void *uin[4] = {x, y, t, p};
+    bool pin_in[4], pin_col[6], pin_echo[4];
+    bool all_pinned = true;
+    for (int k = 0; k < 4; ++k) all_pinned &= (pin_in[k] = is_pinned(uin[k]));
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
+    int32_t *const uecho[4] = {out->x, out->y, out->t, out->p};
+    for (int k = 0; k < 6; ++k) all_pinned &= (pin_col[k] = is_pinned(ucol[k]));
+    for (int k = 0; k < 4; ++k) all_pinned &= (pin_echo[k] = is_pinned(uecho[k]));
+    const bool pin_scale = is_pinned(out->scale);
+    all_pinned &= pin_scale;
+    if (!all_pinned && (rc = ensure_pinned(h, n))) return rc;
+    if (!h->s_copy) HIPCHK(hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking));
+    if (!h->s_up) HIPCHK(hipStreamCreateWithFlags(&h->s_up, hipStreamNonBlocking));
+    const int T = host_threads();
+    // pinned staging: inputs x | y | t | p, records: six double columns, then scale
+    int32_t *stg_in[4];
+    for (int k = 0; k < 4; ++k) stg_in[k] = h->pin_in ? reinterpret_cast<int32_t *>(h->pin_in) + (size_t)k * n : nullptr;
+    const int32_t *src_in[4];
+    for (int k = 0; k < 4; ++k) src_in[k] = pin_in[k] ? static_cast<const int32_t *>(uin[k]) : stg_in[k];
+    double *pcol[6];
+    for (int k = 0; k < 6; ++k) pcol[k] = h->pin_out ? reinterpret_cast<double *>(h->pin_out) + (size_t)k * n : nullptr;
+    int32_t *pscale = h->pin_out ? reinterpret_cast<int32_t *>(reinterpret_cast<double *>(h->pin_out) + 6 * (size_t)n)
+                                 : nullptr;
+    double *dst_col[6];
+    for (int k = 0; k < 6; ++k) dst_col[k] = pin_col[k] ? ucol[k] : pcol[k];
+    int32_t *const dst_scale = pin_scale ? out->scale : pscale;
+    bool any_host_copy = !pin_scale;  // copy-out threads needed
+    for (int k = 0; k < 6; ++k) any_host_copy |= !pin_col[k];
+    for (int k = 0; k < 4; ++k) any_host_copy |= !pin_echo[k];
 
-    // one completion event per pooling super-chunk, created before the worker
-    // threads start: the hook must not grow copy_ev while they read it
+    // one completion event per pooling super-chunk of the call, created before
+    // the copy-out threads start: the hook must not grow copy_ev while they read it
     {
-        const int64_t n_super = ceil_div(ceil_div(n, h->pool_chunk), h->pool_batch);
-        while ((int64_t)h->copy_ev.size() < n_super) {
+        const int64_t n_super_all = (int64_t)nbat * ceil_div(ceil_div(sub, h->pool_chunk), h->pool_batch);
+        while ((int64_t)h->copy_ev.size() < n_super_all) {
             hipEvent_t ev;
             HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             h->copy_ev.push_back(ev);
         }
     }
-    struct Ready { int S, p0, p1; };
+    struct Ready { int64_t S, p0, p1; };
     std::mutex mu;
     std::condition_variable cv;
     std::vector<Ready> ready;
     size_t taken = 0;
     bool closed = false;
     std::atomic<int> bad{0};
-    auto worker = [&]() {
+    auto worker = [&]() {  // pageable records: copy-out of landed super-chunks, with the x, y, t, p echo
         for (;;) {
             Ready r;
             {
@@ -3145,17 +3257,18 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             }
             if (hipEventSynchronize(h->copy_ev[r.S]) != hipSuccess) { bad = 1; continue; }
             const size_t k = (size_t)(r.p1 - r.p0);
-            for (int c = 0; c < 6; ++c) std::memcpy(ucol[c] + r.p0, pcol[c] + r.p0, 8 * k);
-            std::memcpy(out->scale + r.p0, pscale + r.p0, 4 * k);
+            for (int c = 0; c < 6; ++c)
+                if (!pin_col[c]) std::memcpy(ucol[c] + r.p0, pcol[c] + r.p0, 8 * k);
+            if (!pin_scale) std::memcpy(out->scale + r.p0, pscale + r.p0, 4 * k);
             // x, y, t, p columns echo the inputs (vFlow.cpp:370-373)
-            std::memcpy(out->x + r.p0, x + r.p0, 4 * k);
-            std::memcpy(out->y + r.p0, y + r.p0, 4 * k);
-            std::memcpy(out->t + r.p0, t + r.p0, 4 * k);
-            std::memcpy(out->p + r.p0, p + r.p0, 4 * k);
+            for (int c = 0; c < 4; ++c)
+                if (!pin_echo[c])
+                    std::memcpy(uecho[c] + r.p0, static_cast<const int32_t *>(uin[c]) + r.p0, 4 * k);
         }
     };
     std::vector<std::thread> pool;
-    for (int i = 0; i < T; ++i) pool.emplace_back(worker);
+    if (any_host_copy)
+        for (int i = 0; i < T; ++i) pool.emplace_back(worker);
     auto finish = [&](int code) {
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -3163,27 +3276,98 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         }
         cv.notify_all();
         for (auto &w : pool) w.join();
-        return code;
+        int rs = sync_all(h);
+        return code ? code : rs;
     };
-    super_hook hook = [&](int S, int p0, int p1, hipEvent_t done) -> int {
-        if ((int)h->copy_ev.size() <= S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
-        HIPCHK(hipStreamWaitEvent(h->s_copy, done, 0));
-        const size_t k = (size_t)(p1 - p0);
-        for (int c = 0; c < 6; ++c)
-            HIPCHK(hipMemcpyAsync(pcol[c] + p0, dcol[c] + p0, 8 * k, hipMemcpyDeviceToHost, h->s_copy));
-        HIPCHK(hipMemcpyAsync(pscale + p0, d.scale + p0, 4 * k, hipMemcpyDeviceToHost, h->s_copy));
-        HIPCHK(hipEventRecord(h->copy_ev[S], h->s_copy));
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            ready.push_back(Ready{S, p0, p1});
+    int64_t S_all = 0;  // super-chunks of the call so far
+    // asynchronous sub-batches unless the call is profiled (timing and counters
+    // are read back per call)
+    const bool async = !h->profiling && !h->counting;
+    int fit_launches = 0, pool_launches = 0;
+    for (int b = 0; b < nbat && !rc; ++b) {
+        const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
+        Work &w = h->ws[b & 1];
+        // ---- range check (vFlow.cpp:264 indexes the surfaces unchecked) and staging
+        std::atomic<int> oor{0};
+        host_parallel(m, T, [&](int64_t i0, int64_t i1) {
+            const int64_t e0 = a0 + i0, k = i1 - i0;
+            const int xlo = h->X0, xhi = h->X0 + h->WR, H = h->H;
+            int o = 0;
+            for (int64_t e = e0; e < e0 + k; ++e) o |= (x[e] < xlo) | (x[e] >= xhi) | (y[e] < 0) | (y[e] >= H);
+            if (o) oor = 1;
+            for (int c = 0; c < 4; ++c)
+                if (!pin_in[c]) std::memcpy(stg_in[c] + e0, static_cast<const int32_t *>(uin[c]) + e0, 4 * k);
+        });
+        if (oor) { rc = fail(FARMS_EINVAL, "event outside the width x height sensor"); break; }
+        // ---- upload into set b % 2, once its previous call is done with it
+        hipStream_t su = h->s_up;
+        if (w.busy && hipStreamWaitEvent(su, w.done, 0) != hipSuccess) { rc = fail(FARMS_EHIP, "upload wait"); break; }
+        if (hipMemcpyAsync(w.x, src_in[0] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(w.y, src_in[1] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(w.t, src_in[2] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(w.p, src_in[3] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipEventRecord(h->up_ev[b & 1], su) != hipSuccess ||
+            hipStreamWaitEvent(h->stream, h->up_ev[b & 1], 0) != hipSuccess) {
+            rc = fail(FARMS_EHIP, "farms_process: host-to-device copy");
+            break;
         }
-        cv.notify_one();
-        return FARMS_OK;
-    };
-    rc = run_core(h, h->x, h->y, h->t, h->p, n, &d, &hook);
+        // ---- compute, with the record downloads hooked onto each super-chunk
+        farms_records d{};
+        d.r_true = w.o_d[0]; d.theta_true = w.o_d[1]; d.vx = w.o_d[2]; d.vy = w.o_d[3];
+        d.r_local = w.o_d[4]; d.theta_local = w.o_d[5]; d.scale = w.o_scale;
+        double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
+        super_hook hook = [&](int, int p0, int p1, hipEvent_t done) -> int {
+            const int64_t S = S_all++;
+            if ((int64_t)h->copy_ev.size() <= S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
+            hipStream_t sd = h->s_copy;
+            HIPCHK(hipStreamWaitEvent(sd, done, 0));
+            const size_t k = (size_t)(p1 - p0);
+            const int64_t g0 = a0 + p0;
+            for (int c = 0; c < 6; ++c)
+                HIPCHK(hipMemcpyAsync(dst_col[c] + g0, dcol[c] + p0, 8 * k, hipMemcpyDeviceToHost, sd));
+            HIPCHK(hipMemcpyAsync(dst_scale + g0, d.scale + p0, 4 * k, hipMemcpyDeviceToHost, sd));
+            // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
+            const int32_t *dev_in[4] = {w.x, w.y, reinterpret_cast<const int32_t *>(w.t), w.p};
+            for (int c = 0; c < 4; ++c)
+                if (pin_echo[c]) HIPCHK(hipMemcpyAsync(uecho[c] + g0, dev_in[c] + p0, 4 * k, hipMemcpyDeviceToHost, sd));
+            HIPCHK(hipEventRecord(h->copy_ev[S], sd));
+            if (any_host_copy) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    ready.push_back(Ready{S, g0, a0 + p1});
+                }
+                cv.notify_one();
+            }
+            return FARMS_OK;
+        };
+        rc = run_core(h, w, w.x, w.y, w.t, w.p, m, &d, &hook, 0, async, /*validated=*/true);
+        if (rc) break;
+        fit_launches += h->stats.fit_launches;
+        pool_launches += h->stats.pool_launches;
+        // the set is free again once its records are downloaded too
+        if (async && (hipStreamWaitEvent(h->s_copy, w.done, 0) != hipSuccess ||
+                      hipEventRecord(w.done, h->s_copy) != hipSuccess)) {
+            rc = fail(FARMS_EHIP, "farms_process: download join");
+            break;
+        }
+    }
     rc = finish(rc);
     if (rc) return rc;
     if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
-    HIPCHK(hipStreamSynchronize(h->s_copy));
+    h->stats.n_events = n;
+    h->stats.fit_launches = fit_launches;
+    h->stats.pool_launches = pool_launches;
+    return FARMS_OK;
+}
+
+extern "C" int farms_host_alloc(int64_t bytes, void **out) {
+    if (!out || bytes < 0) return fail(FARMS_EINVAL, "bad argument");
+    *out = nullptr;
+    HIPCHK(hipHostMalloc(out, (size_t)(bytes > 0 ? bytes : 1), hipHostMallocDefault));
+    return FARMS_OK;
+}
+
+extern "C" int farms_host_free(void *p) {
+    if (p) HIPCHK(hipHostFree(p));
     return FARMS_OK;
 }

@@ -112,7 +112,7 @@ HIP_SYMBOLS = (
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
     "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
     "farms_seed_sae", "farms_serial_first", "farms_fit_device", "farms_pool_device", "farms_export_flows",
-    "farms_import_flows",
+    "farms_import_flows", "farms_host_alloc", "farms_host_free",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text",
                  "farms_synth_generate_select", "farms_synth_column_hist")
@@ -153,6 +153,8 @@ def load_hip_library() -> ctypes.CDLL:
             getattr(lib, name).restype = ctypes.c_int
     lib.farms_process.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
     lib.farms_process_device.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_void_p]
+    lib.farms_host_alloc.argtypes = [ctypes.c_int64, ctypes.c_void_p]
+    lib.farms_host_free.argtypes = [ctypes.c_void_p]
     _hip = lib
     return lib
 
@@ -213,13 +215,48 @@ class Events:
                 np.ascontiguousarray(t_rel), np.ascontiguousarray(p))
 
 
-class Records:
-    """SoA of the 11 output columns (vFlow.cpp:438)."""
+class PinnedArray:
+    """A numpy array in pinned host memory (farms_host_alloc): farms_process
+    DMAs it in place instead of through its staging."""
 
-    def __init__(self, n: int):
+    def __init__(self, n: int, dtype):
+        lib = load_hip_library()
+        self.dtype = np.dtype(dtype)
+        p = ctypes.c_void_p()
+        _check(lib, lib.farms_host_alloc(ctypes.c_int64(max(n, 1) * self.dtype.itemsize), ctypes.byref(p)))
+        self._p, self._lib = p, lib
+        buf = (ctypes.c_char * (max(n, 1) * self.dtype.itemsize)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=n)
+
+    def __del__(self):
+        if getattr(self, "_p", None) is not None and self._p.value:
+            self._lib.farms_host_free(self._p)
+            self._p = None
+
+
+def pinned(a: np.ndarray):
+    """A pinned copy of `a` and its owner (keep the owner alive while the array is used)."""
+    own = PinnedArray(len(a), a.dtype)
+    own.array[:] = a
+    return own.array, own
+
+
+class Records:
+    """SoA of the 11 output columns (vFlow.cpp:438); pinned=True: in pinned host
+    memory (farms_process then DMAs the records straight into them)."""
+
+    def __init__(self, n: int, pinned: bool = False):
         self.n = n
+        self._owners = []
         for name in COLUMNS:
-            setattr(self, name, np.zeros(n, dtype=np.int32 if name in INT_COLUMNS else np.float64))
+            dt = np.int32 if name in INT_COLUMNS else np.float64
+            if pinned:
+                own = PinnedArray(n, dt)
+                own.array[:] = 0
+                self._owners.append(own)
+                setattr(self, name, own.array)
+            else:
+                setattr(self, name, np.zeros(n, dtype=dt))
 
     def as_c(self) -> FarmsRecordsC:
         return FarmsRecordsC(*[getattr(self, name).ctypes.data for name in COLUMNS])

@@ -14,6 +14,25 @@
 
 #include "event_io.h"
 
+namespace {
+// An array in pinned host memory (farms_host_alloc): farms_process DMAs it in
+// place instead of staging it.
+template <class T>
+struct Pinned {
+    T *ptr = nullptr;
+    explicit Pinned(size_t n) {
+        void *v = nullptr;
+        if (farms_host_alloc((int64_t)(n * sizeof(T)), &v) != FARMS_OK)
+            throw std::runtime_error(std::string("farms_host_alloc: ") + farms_last_error());
+        ptr = static_cast<T *>(v);
+    }
+    ~Pinned() { farms_host_free(ptr); }
+    Pinned(const Pinned &) = delete;
+    Pinned &operator=(const Pinned &) = delete;
+    T &operator[](size_t i) { return ptr[i]; }
+};
+}  // namespace
+
 vFlowManager::vFlowManager(int height, int width, int filterSize, int minEvtsOnPlane)
     : vFlowManager(height, width, filterSize, minEvtsOnPlane, std::string()) {}
 
@@ -73,19 +92,20 @@ long vFlowManager::process(bool write_output) {
     int rc = ensure_handle();
     if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_create: ") + farms_last_error());
 
-    std::vector<uint32_t> t_rel((size_t)n);
-    std::vector<int32_t> p((size_t)n);
-    std::vector<int32_t> ox((size_t)n), oy((size_t)n), ot((size_t)n), op((size_t)n), osc((size_t)n);
-    std::vector<double> rt((size_t)n), tt((size_t)n), vx((size_t)n), vy((size_t)n), rl((size_t)n), tl((size_t)n);
-    farms_records rec{ox.data(), oy.data(), ot.data(), op.data(), rt.data(), tt.data(),
-                      vx.data(), vy.data(), rl.data(), tl.data(), osc.data()};
+    // the loop's own arrays in pinned memory: DMAed in place (X and Y, the
+    // reference's public vectors, go through the library's staging)
+    const size_t un = (size_t)n;
+    Pinned<uint32_t> t_rel(un);
+    Pinned<int32_t> p(un), ox(un), oy(un), ot(un), op(un), osc(un);
+    Pinned<double> rt(un), tt(un), vx(un), vy(un), rl(un), tl(un);
+    farms_records rec{ox.ptr, oy.ptr, ot.ptr, op.ptr, rt.ptr, tt.ptr, vx.ptr, vy.ptr, rl.ptr, tl.ptr, osc.ptr};
 
     const auto start = std::chrono::system_clock::now();  // vFlow.cpp:214
     for (int64_t e = 0; e < n; ++e) {
         t_rel[(size_t)e] = T[(size_t)e] - t0;                   // vFlow.cpp:240-241
         p[(size_t)e] = POL[(size_t)e] < 0 ? 0 : POL[(size_t)e];  // vFlow.cpp:245-247
     }
-    rc = farms_process(handle, X.data(), Y.data(), t_rel.data(), p.data(), n, &rec);
+    rc = farms_process(handle, X.data(), Y.data(), t_rel.ptr, p.ptr, n, &rec);
     const auto stop = std::chrono::system_clock::now();  // vFlow.cpp:416
     if (rc != FARMS_OK) throw std::runtime_error(std::string("farms_process: ") + farms_last_error());
     numEvents += (double)n;

@@ -114,9 +114,19 @@ int farms_reset(farms_handle *h);
 /* Run the per-event loop of runFileCopy (vFlow.cpp:223-414) over n events in
  * stream order.  t_rel is T - t0 as uint32 (vFlow.cpp:240-241); p is the
  * polarity already clamped to >= 0 (vFlow.cpp:245-247) and is only echoed.
- * Host pointers.  Synchronous. */
+ * Host pointers; arrays in pinned memory (farms_host_alloc) are DMAed directly,
+ * others through the handle's pinned staging.  Synchronous.  A long call runs
+ * as a pipeline of sub-batches (bitwise one call); an event outside the sensor
+ * returns FARMS_EINVAL before its sub-batch runs, earlier sub-batches of the
+ * call having been processed (farms_reset to start over). */
 int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t_rel,
                   const int32_t *p, int64_t n, farms_records *out);
+
+/* Pinned (page-locked) host memory for farms_process's inputs and records:
+ * the DMA engines read and write it in place (no staging copy).  Not in the
+ * reference (its vectors are pageable, vFlow.h:111-114). */
+int farms_host_alloc(int64_t bytes, void **out);
+int farms_host_free(void *p);
 
 /* Same with device-resident inputs and outputs (no PCIe traffic).  Synchronous
  * with respect to the handle's stream. */

@@ -291,12 +291,15 @@ def test_full_size_stream_properties():
     assert int((outs[0]["r_local"] > 0).sum()) > n // 4  # most of the stream is pooled
 
 
-@pytest.mark.parametrize("threads,pool_chunk", [("1", 1024), ("3", 2048), ("8", 0)])
-def test_host_path_equals_device_path(threads, pool_chunk, monkeypatch):
-    """farms_process (pinned staging, record downloads overlapped per pooling
-    super-chunk, threaded copy-out) gives bitwise the records of
-    farms_process_device on the same stream, for any thread count and with
-    many super-chunks in flight."""
+@pytest.mark.parametrize("threads,pool_chunk,pin", [("1", 1024, "none"), ("3", 2048, "all"), ("8", 0, "mixed"),
+                                                    ("8", 1024, "all")])
+def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
+    """farms_process (pipelined sub-batches -- several here: the stream is 3M
+    events, a sub-batch at least 4 super-chunks of pool_chunk x pool_batch --,
+    record downloads overlapped per pooling super-chunk, pinned arrays DMAed
+    in place and pageable ones staged) gives bitwise the records of
+    farms_process_device on the same stream, for any thread count and mix of
+    pinned and pageable arrays."""
     import torch
 
     monkeypatch.setenv("FARMS_HOST_THREADS", threads)
@@ -307,13 +310,46 @@ def test_host_path_equals_device_path(threads, pool_chunk, monkeypatch):
     d = [torch.from_numpy(a).to(dev) for a in (x, y, t.view(np.int32), p)]
     o = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
          for c in farms.COLUMNS[4:]}
+    keep = []
+    ins = [x, y, t, p]
+    if pin != "none":
+        for i in ((0, 1, 2, 3) if pin == "all" else (1, 2)):
+            ins[i], own = farms.pinned(ins[i])
+            keep.append(own)
+    rec = farms.Records(n, pinned=pin == "all")
+    if pin == "mixed":  # a pinned record column and a pinned echo column among pageable ones
+        for c in ("vx", "t"):
+            a, own = farms.pinned(getattr(rec, c))
+            setattr(rec, c, a)
+            keep.append(own)
     with farms.FlowManager(720, 1280, 5, 5, pool_chunk=pool_chunk, pool_batch=8 if pool_chunk else 0) as fm:
         fm.process_device(*d, o)
         fm.reset()
-        g = fm.process(x, y, t, p)
+        g = fm.process(*ins, out=rec)
+        fm.reset()
+        g1 = fm.process(x[:777], y[:777], t[:777], p[:777])  # one sub-batch
     dd = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
     dd.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
     assert bitwise_equal(g, dd)
+    assert g1.n == 777 and np.array_equal(g1.scale, dd["scale"][:777])
+
+
+def test_host_path_out_of_sensor_in_a_later_sub_batch():
+    """An event outside the sensor stops a pipelined call before its sub-batch;
+    after a reset the handle processes the stream as if fresh."""
+    ev = farms.synth_config(3, 2_000_000)
+    x, y, t, p = ev.relative()
+    xb = x.copy()
+    xb[-5] = 1280
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
+        with pytest.raises(farms.FarmsError) as ei:
+            fm.process(xb, y, t, p)
+        assert ei.value.code == farms.FARMS_EINVAL
+        fm.reset()
+        a = fm.process(x, y, t, p)
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
+        b = fm.process(x, y, t, p)
+    assert bitwise_equal(a, b)
 
 
 def serial_inputs(ev):

@@ -163,6 +163,7 @@ struct Ctx {
     const int32_t *P;      // event ids sorted by (pixel, id)
     const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
     int4 *qe;              // per work-order position: {event id or -1 if not pooled, x, y, t} (k_pool_desc)
+    int4 *fdesc;           // per work-order position: {event id, x, y, t} (k_fit_desc)
     // per event, one 16-B record (k_link): {position in P, previous and next
     // event at the pixel (-1 / INT_MAX: none), tpv}; tpv = the stamp the
     // pixel's SAE holds just before the event (the previous event's, or, for
@@ -386,10 +387,19 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, in
 __global__ void k_pool_desc(Ctx c, int p0, int p1) {
     const int w = p0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (w >= p1) return;
+    const int4 fd = c.fdesc[w];
+    const bool ok = c.valid[fd.x] && fd.y >= c.own_lo && fd.y < c.own_hi;
+    c.qe[w] = make_int4(ok ? fd.x : -1, fd.y, fd.z, fd.w);
+}
+
+// Fit descriptor per work-order position: {event, x, y, t}, so that a fit
+// wave opens with one 16-B load where it needed two dependent round trips (Q,
+// then the event's fields).  After the work-order sort, in prep.
+__global__ void k_fit_desc(Ctx c) {
+    const int w = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (w >= c.n) return;
     const int e = c.Q[w];
-    const int ex = c.x[e], ey = c.y[e];
-    const bool ok = c.valid[e] && ex >= c.own_lo && ex < c.own_hi;
-    c.qe[w] = make_int4(ok ? e : -1, ex, ey, (int)c.t[e]);
+    c.fdesc[w] = make_int4(e, c.x[e], c.y[e], (int)c.t[e]);
 }
 
 // The prep of one fit chunk as its own launch (the first chunk of a call, the
@@ -581,12 +591,12 @@ __device__ void fit_event_generic(const Ctx &c, int e, uint32_t seq, double &vx_
 // window's stamps go to LDS (`lt`: this thread's column, stride 256) for the
 // three passes over it.  Arithmetic is that of fit_event_generic.
 template <int FR>
-__device__ __forceinline__ void fit_event_fast(const Ctx &c, int e, uint32_t seq, uint32_t *lt, double &vx_out,
+__device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t seq, uint32_t *lt, double &vx_out,
                                                double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
-    const int ex = c.x[e], ey = c.y[e];
-    const uint32_t te = c.t[e];
+    const int e = fd.x, ex = fd.y, ey = fd.z;  // the fit descriptor (k_fit_desc)
+    const uint32_t te = (uint32_t)fd.w;
     vx_out = 0.0;
     vy_out = 0.0;
     acc_out = false;
@@ -831,15 +841,12 @@ __global__ __launch_bounds__(256) void k_fit(Ctx c, int c0, int c1, uint32_t seq
     __shared__ uint32_t s_tk[NPC * 256];
     const int w = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= c1) return;
-    const int e = c.Q[w];  // chunk [c0, c1) occupies positions [c0, c1) of Q
-    if (!c.fit_all) {
-        const int ex = c.x[e];
-        if (ex < c.fit_lo || ex >= c.fit_hi) return;
-    }
+    const int4 fd = c.fdesc[w];  // chunk [c0, c1) occupies positions [c0, c1) of Q
+    if (!c.fit_all && (fd.y < c.fit_lo || fd.y >= c.fit_hi)) return;
     double vx, vy;
     bool acc;
-    fit_event_fast<FR>(c, e, seq, s_tk + threadIdx.x, vx, vy, acc);
-    fit_plane(c, e, vx, vy, acc);
+    fit_event_fast<FR>(c, fd, seq, s_tk + threadIdx.x, vx, vy, acc);
+    fit_plane(c, fd.x, vx, vy, acc);
 }
 
 
@@ -898,12 +905,12 @@ __device__ __forceinline__ uint64_t quad_or_u64(uint64_t v) {
 constexpr int kFitQS = 16;  // quads per fit workgroup: stride of the LDS stamp tiles
 
 template <int FR>
-__device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq, int j, uint32_t *lt, double &vx_out,
+__device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t seq, int j, uint32_t *lt, double &vx_out,
                                                double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
-    const int ex = c.x[e], ey = c.y[e];
-    const uint32_t te = c.t[e];
+    const int e = fd.x, ex = fd.y, ey = fd.z;  // the fit descriptor (k_fit_desc)
+    const uint32_t te = (uint32_t)fd.w;
     vx_out = 0.0;
     vy_out = 0.0;
     acc_out = false;
@@ -1070,12 +1077,12 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int e, uint32_t seq
 // their visited bits to a register mask, so the winning window needs no second
 // round of loads (window column cxo is union column (bw / 3) * FR + cxo).
 template <int FR>
-__device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int e, uint32_t seq, int j, uint32_t *ut, double &vx_out,
+__device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t seq, int j, uint32_t *ut, double &vx_out,
                                                  double &vy_out, bool &acc_out) {
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
-    const int ex = c.x[e], ey = c.y[e];
-    const uint32_t te = c.t[e];
+    const int e = fd.x, ex = fd.y, ey = fd.z;  // the fit descriptor (k_fit_desc)
+    const uint32_t te = (uint32_t)fd.w;
     vx_out = 0.0;
     vy_out = 0.0;
     acc_out = false;
@@ -1264,16 +1271,14 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
-    const int e = c.Q[w];
-    if (!c.fit_all) {  // halo columns: flows come from their owner (farms_import_flows)
-        const int ex = c.x[e];
-        if (ex < c.fit_lo || ex >= c.fit_hi) return;  // the whole quad
-    }
+    const int4 fd = c.fdesc[w];  // {event, x, y, t}: one 16-B load (k_fit_desc)
+    // halo columns: flows come from their owner (farms_import_flows); the whole quad
+    if (!c.fit_all && (fd.y < c.fit_lo || fd.y >= c.fit_hi)) return;
     double vx, vy;
     bool acc;
-    if constexpr (UT) fit_event_quad_u<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
-    else fit_event_quad<FR>(c, e, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
-    if (j == 0) fit_plane(c, e, vx, vy, acc);
+    if constexpr (UT) fit_event_quad_u<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    else fit_event_quad<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    if (j == 0) fit_plane(c, fd.x, vx, vy, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -2222,7 +2227,7 @@ struct Work {
     int2 *PT = nullptr;
     int4 *link = nullptr;
     int32_t *Q = nullptr;
-    int4 *qe = nullptr;
+    int4 *qe = nullptr, *fdesc = nullptr;
     double2 *plane = nullptr;
     uint32_t *wkey = nullptr, *wkey_sorted = nullptr;
     uint8_t *valid = nullptr;
@@ -2311,7 +2316,7 @@ void dfree(T *&p) {
 void free_workspace(Work &w) {
     dfree(w.x); dfree(w.y); dfree(w.p); dfree(w.t); dfree(w.pix); dfree(w.skey);
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
-    dfree(w.Q); dfree(w.qe); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
+    dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.o_scale); dfree(w.ctmin); dfree(w.ctmax);
     for (auto &d : w.o_d) dfree(d);
     dfree(w.cub_tmp);
@@ -2343,7 +2348,7 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
     if ((rc = dalloc(&w.x, cap)) || (rc = dalloc(&w.y, cap)) || (rc = dalloc(&w.p, cap)) ||
         (rc = dalloc(&w.t, cap)) || (rc = dalloc(&w.pix, cap)) || (rc = dalloc(&w.skey, cap)) ||
         (rc = dalloc(&w.iota, cap)) || (rc = dalloc(&w.P, cap)) || (rc = dalloc(&w.PT, cap)) ||
-        (rc = dalloc(&w.link, cap)) || (rc = dalloc(&w.Q, cap)) || (rc = dalloc(&w.qe, cap)) ||
+        (rc = dalloc(&w.link, cap)) || (rc = dalloc(&w.Q, cap)) || (rc = dalloc(&w.qe, cap)) || (rc = dalloc(&w.fdesc, cap)) ||
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
         (rc = dalloc(&w.o_scale, cap)) || (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch))) {
@@ -2488,7 +2493,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.invJ = 1.0f / (float)h->J;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = w.pix; c.skey = w.skey; c.P = w.P; c.link = w.link;
-    c.Q = w.Q; c.qe = w.qe; c.plane = w.plane;
+    c.Q = w.Q; c.qe = w.qe; c.fdesc = w.fdesc; c.plane = w.plane;
     c.cells = h->cells; c.PT = w.PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
     c.pcur = w.pcur; c.pend = w.pend;
@@ -2561,6 +2566,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, b2, w.wkey, w.wkey_sorted, w.iota, w.Q, n, 0,
                                                   h->tile_bits + cb, s));
     }
+    hipLaunchKernelGGL(k_fit_desc, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
@@ -2703,6 +2709,21 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     if (n_super > 0) HIPCHK(hipEventRecord(h->chain_end, sc));
     HIPCHK(hipGetLastError());
     const int pool_launches = n_super;
+    if (async && n_super > 0) {
+        // w.done, on stream P after the last pooling launch (which follows the
+        // chain's last step) and F's last work: the next call's fits on F do not
+        // wait for this call's pooling
+        HIPCHK(hipEventRecord(ev_prep, s));  // (reused: F's end of this call)
+        HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
+        HIPCHK(hipEventRecord(w.done, sp));
+        w.busy = true;
+        farms_stats st{};
+        st.n_events = n;
+        st.fit_launches = fit_launches;
+        st.pool_launches = pool_launches;
+        h->stats = st;
+        return FARMS_OK;
+    }
     // join: stream F waits for the last chain step and the last pooling launch
     if (n_super > 0) {
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));

@@ -3210,8 +3210,19 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     // profiled or counted calls stay one call (their figures are per call)
     const int64_t super = (int64_t)h->pool_chunk * h->pool_batch;
     int64_t sub = n;
-    if (!h->profiling && !h->counting) {
-        const int64_t per = std::max<int64_t>(4 * super, (n / 8 + super - 1) / super * super);
+    const char *sbv = getenv("FARMS_SUBBATCHES");  // A/B aid: 1 = one call, k = about n / k per sub-batch
+    const int64_t nsub = sbv ? std::max(1, atoi(sbv)) : 8;
+    const char *trv = getenv("FARMS_HOST_TRACE");   // 1: host timestamps of the pipeline on stderr
+    const bool trace = trv && trv[0] == '1';
+    const auto tr0 = std::chrono::steady_clock::now();
+    auto tr = [&](const char *what, int b) {
+        if (trace)
+            std::fprintf(stderr, "[farms host] %8.3f ms %s %d\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(),
+                         what, b);
+    };
+    if (!h->profiling && !h->counting && nsub > 1) {
+        const int64_t per = std::max<int64_t>(4 * super, (n / nsub + super - 1) / super * super);
         if (n > 2 * per) sub = per;
     }
     const int nbat = ceil_div(n, sub);
@@ -3227,7 +3238,9 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
     int32_t *const uecho[4] = {out->x, out->y, out->t, out->p};
     for (int k = 0; k < 6; ++k) all_pinned &= (pin_col[k] = is_pinned(ucol[k]));
-    for (int k = 0; k < 4; ++k) all_pinned &= (pin_echo[k] = is_pinned(uecho[k]));
+    const char *edv = getenv("FARMS_ECHO_DMA");  // A/B aid: 0 = the x/y/t/p echo by host copies
+    const bool echo_dma = !(edv && edv[0] == '0');
+    for (int k = 0; k < 4; ++k) all_pinned &= (pin_echo[k] = echo_dma && is_pinned(uecho[k]));
     const bool pin_scale = is_pinned(out->scale);
     all_pinned &= pin_scale;
     if (!all_pinned && (rc = ensure_pinned(h, n))) return rc;
@@ -3319,6 +3332,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             for (int c = 0; c < 4; ++c)
                 if (!pin_in[c]) std::memcpy(stg_in[c] + e0, static_cast<const int32_t *>(uin[c]) + e0, 4 * k);
         });
+        tr("staged", b);
         if (oor) { rc = fail(FARMS_EINVAL, "event outside the width x height sensor"); break; }
         // ---- upload into set b % 2, once its previous call is done with it
         hipStream_t su = h->s_up;
@@ -3365,6 +3379,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         if (rc) break;
         fit_launches += h->stats.fit_launches;
         pool_launches += h->stats.pool_launches;
+        tr("enqueued", b);
         // the set is free again once its records are downloaded too
         if (async && (hipStreamWaitEvent(h->s_copy, w.done, 0) != hipSuccess ||
                       hipEventRecord(w.done, h->s_copy) != hipSuccess)) {
@@ -3372,7 +3387,13 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             break;
         }
     }
+    if (trace) {  // when the device finished each stream's work
+        (void)hipStreamSynchronize(h->stream); tr("F done", nbat);
+        (void)hipStreamSynchronize(h->s_pool); tr("P done", nbat);
+        (void)hipStreamSynchronize(h->s_copy); tr("D2H done", nbat);
+    }
     rc = finish(rc);
+    tr("copy-out done", nbat);
     if (rc) return rc;
     if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
     h->stats.n_events = n;

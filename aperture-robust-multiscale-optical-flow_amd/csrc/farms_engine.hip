@@ -2241,6 +2241,7 @@ struct Work {
     int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
     std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
     hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
+    hipEvent_t ready = nullptr;                // two-phase calls: the fits and the imported flows are in place
     bool busy = false;                         // `done` recorded and the set not yet reused
 };
 
@@ -2270,11 +2271,19 @@ struct farms_handle {
     hipStream_t s_chain = nullptr, s_pool = nullptr;  // candidate-building chain, pooling kernels
     uint32_t seq = 0;
     Work ws[2];
-    // two-phase calls (farms_fit_device / farms_pool_device): phase 1's inputs
-    const int32_t *ph_x = nullptr, *ph_y = nullptr, *ph_p = nullptr;
-    const uint32_t *ph_t = nullptr;
-    int64_t ph_n = -1;
-    farms_records ph_out{};
+    // two-phase calls (farms_fit_device / farms_pool_device): the fits not yet
+    // pooled, oldest first (at most two: the fit of sub-batch b+1 may be issued
+    // before the pooling of b), each on its own workspace set
+    struct Phase {
+        const int32_t *x, *y, *p;
+        const uint32_t *t;
+        int64_t n;
+        farms_records out;
+        int set;
+    };
+    Phase ph[2] = {};
+    int ph_count = 0;
+    uint32_t ph_seq = 0;  // fits issued: the next one's workspace set is ph_seq % 2
     int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
     uint32_t first_t = 0;
     bool fresh = true;          // no event since create / reset (farms_serial_first's precondition)
@@ -2383,6 +2392,7 @@ int reset_surfaces(farms_handle *h) {
     HIPCHK(hipStreamSynchronize(h->stream));
     h->seq = 0;
     h->chunk_base = h->super_base = 0;
+    h->ph_count = 0;  // fits not pooled are dropped
     h->first_q = -1;
     h->fresh = true;
     return FARMS_OK;
@@ -2531,15 +2541,15 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         int rc = ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
         if (rc) return rc;
     }
-    hipEvent_t ev_prep = w.sync_ev[0];
+    hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
     auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
     auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
     auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
 
     // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
-    if (phase == 2) {  // prepared by phase 1
+    if (phase == 2) {  // prepared by phase 1: its fits and the imported flows are in place at w.ready
         if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
-        HIPCHK(hipEventRecord(ev_prep, s));
+        ev_prep = w.ready;
     } else {
     if (!validated) HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err,
@@ -2648,7 +2658,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             if (rc) return rc;
         }
         hipLaunchKernelGGL(k_flow, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, 0, n);
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipEventRecord(w.ready, s));
+        if (!async) HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipGetLastError());
         farms_stats st{};
         st.n_events = n;
@@ -2711,10 +2722,12 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     const int pool_launches = n_super;
     if (async && n_super > 0) {
         // w.done, on stream P after the last pooling launch (which follows the
-        // chain's last step) and F's last work: the next call's fits on F do not
-        // wait for this call's pooling
-        HIPCHK(hipEventRecord(ev_prep, s));  // (reused: F's end of this call)
-        HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
+        // chain's last step) and F's last work of the call (phase 2 has none):
+        // the next call's fits on F do not wait for this call's pooling
+        if (phase != 2) {
+            HIPCHK(hipEventRecord(ev_prep, s));  // (reused: F's end of this call)
+            HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
+        }
         HIPCHK(hipEventRecord(w.done, sp));
         w.busy = true;
         farms_stats st{};
@@ -2896,7 +2909,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     {
         std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->up_ev[0],
-                                         &h->up_ev[1], &h->ws[0].done, &h->ws[1].done};
+                                         &h->up_ev[1], &h->ws[0].done, &h->ws[1].done, &h->ws[0].ready,
+                                         &h->ws[1].ready};
         for (hipEvent_t *ev : evs)
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
                 return bail(fail(FARMS_EHIP, "hipEventCreate"));
@@ -2926,6 +2940,7 @@ extern "C" int farms_destroy(farms_handle *h) {
         dfree(w.pcur); dfree(w.pend);
         for (auto &ev : w.sync_ev) (void)hipEventDestroy(ev);
         if (w.done) (void)hipEventDestroy(w.done);
+        if (w.ready) (void)hipEventDestroy(w.ready);
     }
     for (auto &ev : h->gpool)
         if (ev) (void)hipEventDestroy(ev);
@@ -3067,36 +3082,54 @@ int check_device_call(farms_handle *h, const int32_t *d_x, const int32_t *d_y, c
 }
 }  // namespace
 
+// Two-phase calls pipeline: farms_fit_device enqueues its sub-batch's prep and
+// fits on the next workspace set and returns; the exports / imports act on the
+// most recent fit; farms_pool_device enqueues the pooling of the oldest fit not
+// yet pooled -- asynchronously when a later fit is pending (its fits and the
+// halo exchange then run under this pooling), else it waits for the device.
 extern "C" int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
                                 const int32_t *d_p, int64_t n, farms_records *d_out) {
     int rc = check_device_call(h, d_x, d_y, d_t, d_p, n, d_out);
     if (rc) return rc;
-    h->ph_n = -1;
-    if (n == 0) return FARMS_OK;
+    if (h->ph_count >= 2) return fail(FARMS_EINVAL, "two fits are already waiting for farms_pool_device");
     HIPCHK(hipSetDevice(h->prm.device));
-    if ((rc = ensure_capacity(h, h->ws[0], n))) return rc;
-    if ((rc = run_core(h, h->ws[0], d_x, d_y, d_t, d_p, n, d_out, nullptr, 1))) return rc;
-    h->ph_x = d_x; h->ph_y = d_y; h->ph_t = d_t; h->ph_p = d_p; h->ph_n = n; h->ph_out = *d_out;
+    const int set = (int)(h->ph_seq & 1);
+    Work &w = h->ws[set];
+    if (n > 0) {
+        if ((rc = ensure_capacity(h, w, n))) return rc;
+        if ((rc = run_core(h, w, d_x, d_y, d_t, d_p, n, d_out, nullptr, 1, /*async=*/true))) return rc;
+    }
+    h->ph[h->ph_count++] = farms_handle::Phase{d_x, d_y, d_p, d_t, n, *d_out, set};
+    ++h->ph_seq;
     return FARMS_OK;
 }
 
 extern "C" int farms_pool_device(farms_handle *h) {
     if (!h) return fail(FARMS_EINVAL, "null handle");
-    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_pool_device without a preceding farms_fit_device");
+    if (h->ph_count == 0) return fail(FARMS_EINVAL, "farms_pool_device without a preceding farms_fit_device");
     HIPCHK(hipSetDevice(h->prm.device));
-    const int64_t n = h->ph_n;
-    h->ph_n = -1;
-    return run_core(h, h->ws[0], h->ph_x, h->ph_y, h->ph_t, h->ph_p, n, &h->ph_out, nullptr, 2);
+    const farms_handle::Phase f = h->ph[0];
+    h->ph[0] = h->ph[1];
+    --h->ph_count;
+    const bool ahead = h->ph_count > 0;  // a later fit is pending: stay asynchronous
+    int rc = FARMS_OK;
+    if (f.n > 0) {
+        farms_records out = f.out;
+        rc = run_core(h, h->ws[f.set], f.x, f.y, f.t, f.p, f.n, &out, nullptr, 2, /*async=*/true);
+    }
+    if (!rc && !ahead) rc = sync_all(h);
+    return rc;
 }
 
 extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
     if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
         return fail(FARMS_EINVAL, "bad argument");
-    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_export_flows outside a fit / pool pair");
+    if (h->ph_count == 0) return fail(FARMS_EINVAL, "farms_export_flows outside a fit / pool pair");
     HIPCHK(hipSetDevice(h->prm.device));
+    const farms_handle::Phase &f = h->ph[h->ph_count - 1];
     if (count > 0)
-        hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->ws[0].evf, d_idx,
-                           (int)count, d_flows);
+        hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->ws[f.set].evf,
+                           d_idx, (int)count, d_flows);
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
     return FARMS_OK;
@@ -3105,13 +3138,16 @@ extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t
 extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows) {
     if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
         return fail(FARMS_EINVAL, "bad argument");
-    if (h->ph_n < 0) return fail(FARMS_EINVAL, "farms_import_flows outside a fit / pool pair");
+    if (h->ph_count == 0) return fail(FARMS_EINVAL, "farms_import_flows outside a fit / pool pair");
     HIPCHK(hipSetDevice(h->prm.device));
+    const farms_handle::Phase &f = h->ph[h->ph_count - 1];
+    Work &w = h->ws[f.set];
     Ctx c{};
-    c.t = h->ph_t; c.evf = h->ws[0].evf; c.valid = h->ws[0].valid;
+    c.t = f.t; c.evf = w.evf; c.valid = w.valid;
     if (count > 0)
         hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, c, d_idx, (int)count,
                            d_flows);
+    HIPCHK(hipEventRecord(w.ready, h->stream));  // the pooling of this fit waits for its imports
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
     return FARMS_OK;

@@ -120,8 +120,9 @@ def make_share(sp, split: str, world: int, rank: int, fs: int, max_window: int, 
     hl, hr = strips.halo(fs, max_window, W, H, exchange=exch)
     if exch:
         sh.lists = strips.exchange_lists(x, plan, rank)
-        sh.label = (f"{world} x-strips: each rank fits its owned columns and, per step, sends the local flows of "
-                    f"its events in other ranks' halos ({hl} / {hr} columns) with one grouped send/recv")
+        sh.label = (f"{world} x-strips: each rank fits its owned columns and sends the local flows of its events in "
+                    f"other ranks' halos ({hl} / {hr} columns) with one grouped send/recv per sub-batch, the fit and "
+                    f"exchange of sub-batch b+1 under the pooling of b")
     else:
         sh.label = f"{world} x-strips, halos of {hl} / {hr} columns recomputed, no data-path collective"
     return sh
@@ -139,9 +140,15 @@ class Stepper:
     """One step of the hot path on a rank: the per-event loop over the share,
     with the split's exchange.  Tensors live on `device` (the GPU for the HIP
     engine, the CPU for the oracle); `xdev` is where collectives run (the GPU
-    under RCCL, the CPU under gloo)."""
+    under RCCL, the CPU under gloo).
 
-    def __init__(self, eng, sh: Share, dist, device, xdev):
+    x-strips with the flow exchange run the step as a pipeline of `nsub`
+    sub-batches cut at the same stream indices on every rank (so the per-
+    sub-batch exchange lists pair up): the fit of sub-batch b+1 and its
+    exchange run while the pooling of b does (farms_fit_device /
+    farms_pool_device pipeline); consecutive sub-batches are bitwise one call."""
+
+    def __init__(self, eng, sh: Share, dist, device, xdev, nsub: int = 8):
         import torch
 
         self.eng, self.sh, self.dist = eng, sh, dist
@@ -162,6 +169,22 @@ class Stepper:
             same = xdev == device
             self.send_x = self.send_buf if same else {q: v.to(xdev) for q, v in self.send_buf.items()}
             self.recv_x = self.recv_buf if same else {q: v.to(xdev) for q, v in self.recv_buf.items()}
+            # sub-batches [lo, hi) of the stored events, cut at stream indices
+            # G_b = b * n_stream / nsub; per sub-batch and peer the slices of
+            # the exchange lists and buffers, indices local to the sub-batch
+            nsub = max(1, min(nsub, sh.n)) if sh.n else 1
+            cuts = np.searchsorted(sh.gidx, [b * sh.n_stream // nsub for b in range(nsub + 1)])
+            cuts[-1] = sh.n
+            self.sub = []
+            for b in range(nsub):
+                lo, hi = int(cuts[b]), int(cuts[b + 1])
+                parts = {}
+                for q, (a, r) in L.items():
+                    s0, s1 = np.searchsorted(a, [lo, hi])
+                    r0, r1 = np.searchsorted(r, [lo, hi])
+                    parts[q] = (torch.from_numpy(a[s0:s1] - lo).to(device), torch.from_numpy(r[r0:r1] - lo).to(device),
+                                slice(int(s0), int(s1)), slice(int(r0), int(r1)))
+                self.sub.append((lo, hi, parts))
         if sh.seg is not None:  # stamp surfaces: this rank's [head, full], everyone's, the merged SAE
             WH = sh.width * sh.height
             self.mine = torch.empty((2, WH), dtype=torch.int64, device=device)
@@ -187,18 +210,34 @@ class Stepper:
         eng, sh, d = self.eng, self.sh, self.dist
         eng.reset()
         if sh.lists is not None:
-            eng.fit_device(self.dx, self.dy, self.dt, self.dp, self.out)
-            for q in sh.lists:
-                eng.export_flows(self.send_idx[q], self.send_buf[q])
-                if self.send_x[q] is not self.send_buf[q]:
-                    self.send_x[q].copy_(self.send_buf[q])
-            strips.exchange(d, sh.lists, self.send_x, self.recv_x)
-            self._sync()
-            for q in sh.lists:
-                if self.recv_x[q] is not self.recv_buf[q]:
-                    self.recv_buf[q].copy_(self.recv_x[q])
-                eng.import_flows(self.recv_idx[q], self.recv_buf[q])
-            eng.pool_device()
+            def fit(b):
+                lo, hi, _ = self.sub[b]
+                eng.fit_device(self.dx[lo:hi], self.dy[lo:hi], self.dt[lo:hi], self.dp[lo:hi],
+                               {c: v[lo:hi] for c, v in self.out.items()})
+
+            def exchange(b):
+                _, _, parts = self.sub[b]
+                sx, rx = {}, {}
+                for q, (si, ri, ss, rs) in parts.items():
+                    eng.export_flows(si, self.send_buf[q][ss])
+                    if self.send_x[q] is not self.send_buf[q]:
+                        self.send_x[q][ss].copy_(self.send_buf[q][ss])
+                    sx[q], rx[q] = self.send_x[q][ss], self.recv_x[q][rs]
+                strips.exchange(d, sh.lists, sx, rx)
+                self._sync()
+                for q, (si, ri, ss, rs) in parts.items():
+                    if self.recv_x[q] is not self.recv_buf[q]:
+                        self.recv_buf[q][rs].copy_(self.recv_x[q][rs])
+                    eng.import_flows(ri, self.recv_buf[q][rs])
+
+            fit(0)
+            exchange(0)
+            for b in range(len(self.sub)):
+                if b + 1 < len(self.sub):
+                    fit(b + 1)  # under the pooling of b
+                eng.pool_device()
+                if b + 1 < len(self.sub):
+                    exchange(b + 1)
             return
         if sh.seg is not None:
             o = sh.seg.n_warm  # the segment's own events start after the warm-up

@@ -135,13 +135,18 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
                          farms_records *d_out);
 
 /* The per-event loop split at its one exchange point (x-strips):
- * farms_fit_device runs prep and the local fits (of the owned columns when
- * import_halo is set) over n device events; farms_export_flows /
- * farms_import_flows move the flows {L, L cos theta, L sin theta} (3 doubles
+ * farms_fit_device enqueues prep and the local fits (of the owned columns when
+ * import_halo is set) over n device events; farms_export_flows (synchronous)
+ * / farms_import_flows move the flows {L, L cos theta, L sin theta} (3 doubles
  * per listed event, d_idx = indices into those n events) out of / into the
- * handle; farms_pool_device then runs the pooling sweep over the same events
- * into the same records.  Equivalent to farms_process_device when nothing is
- * imported.  Records of non-owned events are left unspecified. */
+ * handle for its most recent fit; farms_pool_device runs the pooling sweep of
+ * the oldest fit not yet pooled into its records.  A stream may be fed in
+ * sub-batches, and the fit (and exchange) of sub-batch b+1 may be issued before
+ * the pooling of b (at most two fits pending): that pooling then runs
+ * asynchronously under them; a farms_pool_device with no later fit pending
+ * waits for the device.  Equivalent to farms_process_device when nothing is
+ * imported.  Records of non-owned events are left unspecified; a halo flow
+ * never imported counts as invalid. */
 int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t_rel,
                      const int32_t *d_p, int64_t n, farms_records *d_out);
 int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows);

@@ -37,13 +37,15 @@ class OracleEngine:
 
     def reset(self):
         self.sae = None
-        self.ev = None
+        self.fitter = OracleFlow(*self.args)   # SAE state across the sub-batches of a step
+        self.pooler = OracleFlow(*self.args)   # flow state across them
+        self.pending = []                      # fits not yet pooled, oldest first
 
     def _oracle(self):
-        o = OracleFlow(*self.args)
         if self.sae is not None:
-            o.seed_sae(self.sae)
-        return o
+            self.fitter.seed_sae(self.sae)
+            self.sae = None
+        return self.fitter
 
     @staticmethod
     def _np(x, y, t, p):
@@ -62,34 +64,34 @@ class OracleEngine:
         out.copy_(torch.from_numpy(segments.merge_np(list(stack.numpy()))))
 
     def process_device(self, x, y, t, p, out):
-        r = self._oracle().process(*self._np(x, y, t, p))
+        r = self._oracle().process(*self._np(x, y, t, p))  # (one call per step)
         for c in COLS[4:]:
             out[c].copy_(torch.from_numpy(r[c]))
 
     def fit_device(self, x, y, t, p, out):
-        self.ev, self.out = self._np(x, y, t, p), out
-        self.fit = self._oracle().process(*self.ev)  # halo events' flows are replaced by imports
-        xs = self.ev[0]
+        ev = self._np(x, y, t, p)
+        fit = self._oracle().process(*ev)  # halo events' flows are replaced by imports
+        xs = ev[0]
         own = (xs >= self.owned[0]) & (xs < self.owned[1]) if self.import_halo else np.ones(len(xs), bool)
-        self.L = np.where(own, self.fit["r_local"], 0.0)
-        self.th = np.where(own, self.fit["theta_local"], 0.0)
-        self.valid = own & gate(self.fit["vx"], self.fit["vy"])
+        self.pending.append({"ev": ev, "out": out, "fit": fit, "L": np.where(own, fit["r_local"], 0.0),
+                             "th": np.where(own, fit["theta_local"], 0.0), "valid": own & gate(fit["vx"], fit["vy"])})
 
     def export_flows(self, idx, buf):
-        i = idx.numpy()
-        buf.copy_(torch.from_numpy(np.stack([self.L[i], self.th[i], self.valid[i].astype(np.float64)], axis=1)))
+        f, i = self.pending[-1], idx.numpy()
+        buf.copy_(torch.from_numpy(np.stack([f["L"][i], f["th"][i], f["valid"][i].astype(np.float64)], axis=1)))
 
     def import_flows(self, idx, buf):
-        i, b = idx.numpy(), buf.numpy()
-        self.L[i], self.th[i], self.valid[i] = b[:, 0], b[:, 1], b[:, 2] > 0
+        f, i, b = self.pending[-1], idx.numpy(), buf.numpy()
+        f["L"][i], f["th"][i], f["valid"][i] = b[:, 0], b[:, 1], b[:, 2] > 0
 
     def pool_device(self):
-        x, y, t, _ = self.ev
-        r = self._oracle().pool_given(x, y, t, self.valid, self.L, self.th)
+        f = self.pending.pop(0)
+        x, y, t, _ = f["ev"]
+        r = self.pooler.pool_given(x, y, t, f["valid"], f["L"], f["th"])
         for c in ("vx", "vy", "r_local", "theta_local"):
-            self.out[c].copy_(torch.from_numpy(self.fit[c]))
+            f["out"][c].copy_(torch.from_numpy(f["fit"][c]))
         for c in ("r_true", "theta_true", "scale"):
-            self.out[c].copy_(torch.from_numpy(r[c]))
+            f["out"][c].copy_(torch.from_numpy(r[c]))
 
 
 def _free_port():
@@ -98,7 +100,7 @@ def _free_port():
         return sock.getsockname()[1]
 
 
-def _rank_main(rank, world, port, cfg, per_rank, split, q):
+def _rank_main(rank, world, port, cfg, per_rank, split, q, engine="oracle"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     fs, maxw = 5, 50
@@ -107,9 +109,13 @@ def _rank_main(rank, world, port, cfg, per_rank, split, q):
     hist = multirank.column_hist(sp, dist, rank) if split != "segments" else None
     sh = multirank.make_share(sp, split, world, rank, fs, maxw, hist)
     W, H = int(sp.width), int(sp.height)
-    eng = OracleEngine(H, W, fs, maxw=maxw, **multirank.engine_args(sh))
     cpu = torch.device("cpu")
-    st = multirank.Stepper(eng, sh, dist, cpu, cpu)
+    if engine == "hip":  # every rank on device 0, collectives over gloo on the CPU
+        eng = farms.FlowManager(H, W, fs, 5, max_window=maxw, device=0, **multirank.engine_args(sh))
+        st = multirank.Stepper(eng, sh, dist, torch.device("cuda", 0), cpu)
+    else:
+        eng = OracleEngine(H, W, fs, maxw=maxw, **multirank.engine_args(sh))
+        st = multirank.Stepper(eng, sh, dist, cpu, cpu)
     st.step()
     merged = multirank.gather_owned(dist, st.owned_records(), sh.n_stream)
     if rank == 0:
@@ -144,6 +150,33 @@ def test_gloo_ranks_with_the_oracle_engine_reproduce_the_whole_run(split, world,
     assert rep["ok"], rep
     for b in rep["boundaries"]:
         assert b["events"] > 0 and b["valid_events"] > 0 and b["bitwise_vs_cr_oracle"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split,world", [("strips", 2), ("segments", 3), ("strips", 3), ("strips-recompute", 2)])
+def test_gloo_ranks_with_the_hip_engine_reproduce_the_whole_run(split, world):
+    """The same plumbing with the HIP engine, every rank on device 0: the merged
+    owned records equal one whole-stream engine run bitwise (the x-strip step is
+    the pipelined one: fit and exchange of sub-batch b+1 under the pooling of b)."""
+    cfg, per_rank = 3, 120_000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, cfg, per_rank, split, q, "hip"))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    merged, info, label = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert merged is not None
+    sp = farms.synth_params(cfg)
+    sp.n_events = per_rank * world
+    x, y, t, p = farms.synth_generate(sp).relative()
+    with farms.FlowManager(720, 1280, 5, 5) as fm:
+        whole = fm.process(x, y, t, p)
+    assert bitwise_equal(merged, whole)
 
 
 def test_boundary_events_of_a_strip_border_reach_both_ways():

@@ -2221,8 +2221,7 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // sub-batch b's sweeps still read set b % 2.
 struct Work {
     int64_t cap = 0;
-    int32_t *x = nullptr, *y = nullptr, *p = nullptr;  // device copies of host inputs (farms_process)
-    uint32_t *t = nullptr, *pix = nullptr, *skey = nullptr;
+    uint32_t *pix = nullptr, *skey = nullptr;
     int32_t *iota = nullptr, *P = nullptr;
     int2 *PT = nullptr;
     int4 *link = nullptr;
@@ -2233,8 +2232,6 @@ struct Work {
     uint8_t *valid = nullptr;
     FlowCell *evf = nullptr;
     int2 *dbg_tc = nullptr;
-    double *o_d[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // records (farms_process)
-    int32_t *o_scale = nullptr;
     uint32_t *ctmin = nullptr, *ctmax = nullptr;
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
@@ -2303,6 +2300,13 @@ struct farms_handle {
     // sub-batch upload
     uint8_t *pin_in = nullptr, *pin_out = nullptr;
     int64_t pin_cap = 0;
+    // the call's device copies of the inputs and its device records, whole-call
+    // sized (sub-batches are slices): a workspace set's reuse never waits for
+    // an upload or a download
+    int32_t *io_x = nullptr, *io_y = nullptr, *io_t = nullptr, *io_p = nullptr;  // (t as its bits)
+    double *io_rec[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    int32_t *io_scale = nullptr;
+    int64_t io_cap = 0;
     hipStream_t s_copy = nullptr, s_up = nullptr;
     std::vector<hipEvent_t> copy_ev;
     hipEvent_t up_ev[2] = {};
@@ -2323,11 +2327,10 @@ void dfree(T *&p) {
 }
 
 void free_workspace(Work &w) {
-    dfree(w.x); dfree(w.y); dfree(w.p); dfree(w.t); dfree(w.pix); dfree(w.skey);
+    dfree(w.pix); dfree(w.skey);
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
-    dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.o_scale); dfree(w.ctmin); dfree(w.ctmax);
-    for (auto &d : w.o_d) dfree(d);
+    dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -2354,18 +2357,15 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
     free_workspace(w);
     const int64_t cap = n;
     const int64_t nch = (cap + h->pool_chunk - 1) / h->pool_chunk;
-    if ((rc = dalloc(&w.x, cap)) || (rc = dalloc(&w.y, cap)) || (rc = dalloc(&w.p, cap)) ||
-        (rc = dalloc(&w.t, cap)) || (rc = dalloc(&w.pix, cap)) || (rc = dalloc(&w.skey, cap)) ||
+    if ((rc = dalloc(&w.pix, cap)) || (rc = dalloc(&w.skey, cap)) ||
         (rc = dalloc(&w.iota, cap)) || (rc = dalloc(&w.P, cap)) || (rc = dalloc(&w.PT, cap)) ||
         (rc = dalloc(&w.link, cap)) || (rc = dalloc(&w.Q, cap)) || (rc = dalloc(&w.qe, cap)) || (rc = dalloc(&w.fdesc, cap)) ||
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
-        (rc = dalloc(&w.o_scale, cap)) || (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch))) {
+        (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch))) {
         free_workspace(w);
         return rc;
     }
-    for (auto &d : w.o_d)
-        if ((rc = dalloc(&d, cap))) { free_workspace(w); return rc; }
     size_t bytes = 0, bytes2 = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, w.pix, w.skey, w.iota, w.P, (int)cap, 0,
                                               end_bit_for(h->WH), h->stream));
@@ -2957,6 +2957,8 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_up) (void)hipStreamDestroy(h->s_up);
     if (h->pin_in) (void)hipHostFree(h->pin_in);
     if (h->pin_out) (void)hipHostFree(h->pin_out);
+    dfree(h->io_x); dfree(h->io_y); dfree(h->io_t); dfree(h->io_p); dfree(h->io_scale);
+    for (auto &d : h->io_rec) dfree(d);
     if (h->s_pool) (void)hipStreamDestroy(h->s_pool);
     if (h->s_chain) (void)hipStreamDestroy(h->s_chain);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -3189,6 +3191,22 @@ int ensure_pinned(farms_handle *h, int64_t n) {
     return FARMS_OK;
 }
 
+int ensure_io(farms_handle *h, int64_t n) {
+    if (n <= h->io_cap) return FARMS_OK;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    dfree(h->io_x); dfree(h->io_y); dfree(h->io_t); dfree(h->io_p); dfree(h->io_scale);
+    for (auto &d : h->io_rec) dfree(d);
+    h->io_cap = 0;
+    if ((rc = dalloc(&h->io_x, n)) || (rc = dalloc(&h->io_y, n)) || (rc = dalloc(&h->io_t, n)) ||
+        (rc = dalloc(&h->io_p, n)) || (rc = dalloc(&h->io_scale, n)))
+        return rc;
+    for (auto &d : h->io_rec)
+        if ((rc = dalloc(&d, n))) return rc;
+    h->io_cap = n;
+    return FARMS_OK;
+}
+
 // Host memory the DMA engines reach directly (hipHostMalloc'd or registered):
 // such arrays skip the pinned staging copy.
 bool is_pinned(const void *p) {
@@ -3264,6 +3282,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     const int nbat = ceil_div(n, sub);
     int rc = ensure_capacity(h, h->ws[0], sub);
     if (!rc && nbat > 1) rc = ensure_capacity(h, h->ws[1], sub);
+    if (!rc) rc = ensure_io(h, n);
     if (rc) return rc;
     // per array: pinned host memory is DMAed directly, pageable memory goes
     // through the handle's pinned staging
@@ -3370,13 +3389,13 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         });
         tr("staged", b);
         if (oor) { rc = fail(FARMS_EINVAL, "event outside the width x height sensor"); break; }
-        // ---- upload into set b % 2, once its previous call is done with it
+        // ---- upload (the call's device copies: nothing to wait for)
         hipStream_t su = h->s_up;
-        if (w.busy && hipStreamWaitEvent(su, w.done, 0) != hipSuccess) { rc = fail(FARMS_EHIP, "upload wait"); break; }
-        if (hipMemcpyAsync(w.x, src_in[0] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(w.y, src_in[1] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(w.t, src_in[2] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(w.p, src_in[3] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+        int32_t *const dev_in[4] = {h->io_x + a0, h->io_y + a0, h->io_t + a0, h->io_p + a0};
+        if (hipMemcpyAsync(dev_in[0], src_in[0] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(dev_in[1], src_in[1] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(dev_in[2], src_in[2] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
+            hipMemcpyAsync(dev_in[3], src_in[3] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
             hipEventRecord(h->up_ev[b & 1], su) != hipSuccess ||
             hipStreamWaitEvent(h->stream, h->up_ev[b & 1], 0) != hipSuccess) {
             rc = fail(FARMS_EHIP, "farms_process: host-to-device copy");
@@ -3384,8 +3403,9 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         }
         // ---- compute, with the record downloads hooked onto each super-chunk
         farms_records d{};
-        d.r_true = w.o_d[0]; d.theta_true = w.o_d[1]; d.vx = w.o_d[2]; d.vy = w.o_d[3];
-        d.r_local = w.o_d[4]; d.theta_local = w.o_d[5]; d.scale = w.o_scale;
+        d.r_true = h->io_rec[0] + a0; d.theta_true = h->io_rec[1] + a0; d.vx = h->io_rec[2] + a0;
+        d.vy = h->io_rec[3] + a0; d.r_local = h->io_rec[4] + a0; d.theta_local = h->io_rec[5] + a0;
+        d.scale = h->io_scale + a0;
         double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
         super_hook hook = [&](int, int p0, int p1, hipEvent_t done) -> int {
             const int64_t S = S_all++;
@@ -3398,7 +3418,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
                 HIPCHK(hipMemcpyAsync(dst_col[c] + g0, dcol[c] + p0, 8 * k, hipMemcpyDeviceToHost, sd));
             HIPCHK(hipMemcpyAsync(dst_scale + g0, d.scale + p0, 4 * k, hipMemcpyDeviceToHost, sd));
             // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
-            const int32_t *dev_in[4] = {w.x, w.y, reinterpret_cast<const int32_t *>(w.t), w.p};
             for (int c = 0; c < 4; ++c)
                 if (pin_echo[c]) HIPCHK(hipMemcpyAsync(uecho[c] + g0, dev_in[c] + p0, 4 * k, hipMemcpyDeviceToHost, sd));
             HIPCHK(hipEventRecord(h->copy_ev[S], sd));
@@ -3411,17 +3430,12 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             }
             return FARMS_OK;
         };
-        rc = run_core(h, w, w.x, w.y, w.t, w.p, m, &d, &hook, 0, async, /*validated=*/true);
+        rc = run_core(h, w, dev_in[0], dev_in[1], reinterpret_cast<const uint32_t *>(dev_in[2]), dev_in[3], m, &d,
+                      &hook, 0, async, /*validated=*/true);
         if (rc) break;
         fit_launches += h->stats.fit_launches;
         pool_launches += h->stats.pool_launches;
         tr("enqueued", b);
-        // the set is free again once its records are downloaded too
-        if (async && (hipStreamWaitEvent(h->s_copy, w.done, 0) != hipSuccess ||
-                      hipEventRecord(w.done, h->s_copy) != hipSuccess)) {
-            rc = fail(FARMS_EHIP, "farms_process: download join");
-            break;
-        }
     }
     if (trace) {  // when the device finished each stream's work
         (void)hipStreamSynchronize(h->stream); tr("F done", nbat);

@@ -2487,6 +2487,46 @@ int ensure_sync_events(Work &w, size_t count) {
 // flow snapshots and cursors, P), the candidate ring continues by chunk number,
 // and `validated` skips the device-side range check (and its host sync).
 typedef std::function<int(int S, int p0, int p1, hipEvent_t done)> super_hook;
+// FARMS_HOST_TRACE=2: host timestamps of run_core's enqueue steps on stderr (diagnostic)
+// FARMS_HOST_TRACE=3: per-callsite host time of the enqueue calls (diagnostic)
+static const char *const kEnqSite[] = {"fit launch", "prep launch", "record ev_fit", "C wait gpool", "C wait ev_fit",
+                                       "k_flow launch", "k_chain launch", "k_pool_desc launch", "record ev_cand",
+                                       "P wait ev_cand", "k_pool launch", "k_true_polar launch", "record ev_pool",
+                                       "record gpool", "D2H wait", "D2H memcpy", "D2H record"};
+static double g_enq_us[17];
+static long g_enq_n[17];
+static bool enq_prof() {
+    static const char *v = getenv("FARMS_HOST_TRACE");
+    return v && v[0] == '3';
+}
+static void enq_report() {
+    if (!enq_prof()) return;
+    for (int i = 0; i < 17; ++i)
+        if (g_enq_n[i])
+            std::fprintf(stderr, "[farms enq] %-22s %7ld calls %10.1f us total %8.2f us/call\n", kEnqSite[i], g_enq_n[i],
+                         g_enq_us[i], g_enq_us[i] / g_enq_n[i]);
+    std::memset(g_enq_us, 0, sizeof(g_enq_us));
+    std::memset(g_enq_n, 0, sizeof(g_enq_n));
+}
+#define ENQ(id, stmt)                                                                                            \
+    do {                                                                                                        \
+        if (enq_prof()) {                                                                                       \
+            const auto enq_t0 = std::chrono::steady_clock::now();                                               \
+            stmt;                                                                                               \
+            g_enq_us[id] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - enq_t0).count(); \
+            ++g_enq_n[id];                                                                                      \
+        } else {                                                                                                \
+            stmt;                                                                                               \
+        }                                                                                                       \
+    } while (0)
+static void enqueue_trace(const char *what, int64_t a, int64_t b) {
+    static const char *v = getenv("FARMS_HOST_TRACE");
+    if (!v || v[0] != '2') return;
+    static const auto t0 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[farms enq] %9.3f ms %s %lld %lld\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), what,
+                 (long long)a, (long long)b);
+}
 int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
              int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0,
              bool async = false, bool validated = false) {
@@ -2580,6 +2620,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
+    enqueue_trace("prep", h->super_base, n);
     }  // prep
 
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
@@ -2629,14 +2670,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f], s));
         bool merged = false;
         if (fast_fit) {
-            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
+            ENQ(0, merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next));
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, w.Q + c0,
                                c1 - c0);
         }
-        if (!merged && next.blocks > 0) launch_prep(next);
+        if (!merged && next.blocks > 0) ENQ(1, launch_prep(next));
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
-        HIPCHK(hipEventRecord(ev_fit(f), s));
+        ENQ(2, HIPCHK(hipEventRecord(ev_fit(f), s)));
         ++fit_launches;
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
             FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
@@ -2675,37 +2716,41 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         // keep the fit sweep one super-chunk ahead of the chain
         const int need = std::min(n_fit_chunks, ceil_div(std::min<int64_t>((int64_t)(ch1 + B) * h->pool_chunk, n),
                                                          h->fit_chunk));
+        enqueue_trace("super", Sg, fit_enqueued);
         while (fit_enqueued < need) {
             int rc = enqueue_fit(fit_enqueued++);
             if (rc) return rc;
         }
+        enqueue_trace("fits", Sg, fit_enqueued);
         // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
-        if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
+        if (Sg >= 2) ENQ(3, HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0)));
         {  // the chain reads the local flows of every event of the super-chunk
             const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
             const int fl = std::min(f, n_fit_chunks - 1);
-            if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
+            if (fl > fit_waited) { ENQ(4, HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0))); fit_waited = fl; }
         }
         if (phase != 2) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
+            ENQ(5, hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1));
         }
         for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
-            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1));
+            ENQ(6, hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1)));
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-            hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
+            ENQ(7, hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1));
         }
-        HIPCHK(hipEventRecord(ev_cand(S), sc));
-        HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
+        ENQ(8, HIPCHK(hipEventRecord(ev_cand(S), sc)));
+        enqueue_trace("chain", Sg, 0);
+        ENQ(9, HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0)));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
-        pl(c, p0, p1, sp);
+        ENQ(10, pl(c, p0, p1, sp));
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
-        hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
-        HIPCHK(hipEventRecord(ev_pool(S), sp));
-        HIPCHK(hipEventRecord(h->gpool[Sg % 3], sp));
+        ENQ(11, hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1));
+        ENQ(12, HIPCHK(hipEventRecord(ev_pool(S), sp)));
+        ENQ(13, HIPCHK(hipEventRecord(h->gpool[Sg % 3], sp)));
+        enqueue_trace("pool", Sg, 0);
         if (on_super) {
             int rc = (*on_super)(S, p0, p1, ev_pool(S));
             if (rc) return rc;
@@ -3209,6 +3254,78 @@ int ensure_io(farms_handle *h, int64_t n) {
 
 // Host memory the DMA engines reach directly (hipHostMalloc'd or registered):
 // such arrays skip the pinned staging copy.
+// Record download of the host path as a kernel: device columns -> pinned host
+// memory (stores over PCIe).  The runtime's own device-to-host copies are
+// blit kernels too, but eleven per super-chunk, each of 256 512-thread
+// workgroups, and under direct dispatch they fell 95 ms behind the compute at
+// C3; one launch of a few workgroups per super-chunk keeps pace with it.
+struct ExportCols {
+    const double *src[6];
+    double *dst[6];
+    const int32_t *srci[5];  // scale, then the x, y, t, p echo
+    int32_t *dsti[5];        // (nullptr: not exported)
+    int64_t n;
+    int vec;                 // every pointer 16-B aligned: double2 / int4 moves (2: nontemporal doubles)
+};
+
+__global__ __launch_bounds__(256) void k_export(ExportCols e) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e.vec) {
+        const int64_t n2 = e.n / 2, n4 = e.n / 4;
+        for (int64_t i = t0; i < n2; i += stride) {
+            double2 v[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) v[c] = reinterpret_cast<const double2 *>(e.src[c])[i];
+            if (e.vec == 2) {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    __builtin_nontemporal_store(v[c].x, e.dst[c] + 2 * i);
+                    __builtin_nontemporal_store(v[c].y, e.dst[c] + 2 * i + 1);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) reinterpret_cast<double2 *>(e.dst[c])[i] = v[c];
+            }
+        }
+        for (int64_t i = t0; i < n4; i += stride) {
+#pragma unroll
+            for (int c = 0; c < 5; ++c)
+                if (e.dsti[c]) reinterpret_cast<int4 *>(e.dsti[c])[i] = reinterpret_cast<const int4 *>(e.srci[c])[i];
+        }
+        if (t0 == 0) {  // tails
+            for (int64_t i = 2 * n2; i < e.n; ++i)
+                for (int c = 0; c < 6; ++c) e.dst[c][i] = e.src[c][i];
+            for (int64_t i = 4 * n4; i < e.n; ++i)
+                for (int c = 0; c < 5; ++c)
+                    if (e.dsti[c]) e.dsti[c][i] = e.srci[c][i];
+        }
+        return;
+    }
+    for (int64_t i = t0; i < e.n; i += stride) {
+        double v[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) v[c] = e.src[c][i];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) e.dst[c][i] = v[c];
+#pragma unroll
+        for (int c = 0; c < 5; ++c)
+            if (e.dsti[c]) e.dsti[c][i] = e.srci[c][i];
+    }
+}
+
+// the device address of pinned host memory (that of a hipHostRegister-ed
+// range may differ from its host address)
+template <class T>
+T *device_view(T *p) {
+    hipPointerAttribute_t a{};
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return p;
+    }
+    return a.devicePointer ? static_cast<T *>(a.devicePointer) : p;
+}
+
 bool is_pinned(const void *p) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -3242,7 +3359,9 @@ void host_parallel(int64_t n, int T, Fn &&fn) {
 //     sub-batch b - 1 (run_core enqueues asynchronously);
 //   compute: run_core on set b % 2, chained on the streams behind b - 1;
 //   download: as each pooling super-chunk's records become final on the
-//     device (run_core's hook) its columns are DMAed -- straight into the
+//     device (run_core's hook; enqueued behind the next sub-batch's upload,
+//     since the two copy streams may share a hardware queue) its columns are
+//     DMAed -- straight into the
 //     caller's arrays when they are pinned (with the x, y, t, p echo from the
 //     device copies), else into pinned staging, moved to the caller's arrays
 //     (with the echo) by host threads as each DMA lands.
@@ -3267,7 +3386,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     const char *sbv = getenv("FARMS_SUBBATCHES");  // A/B aid: 1 = one call, k = about n / k per sub-batch
     const int64_t nsub = sbv ? std::max(1, atoi(sbv)) : 8;
     const char *trv = getenv("FARMS_HOST_TRACE");   // 1: host timestamps of the pipeline on stderr
-    const bool trace = trv && trv[0] == '1';
+    const bool trace = trv && (trv[0] >= '1' && trv[0] <= '3');
     const auto tr0 = std::chrono::steady_clock::now();
     auto tr = [&](const char *what, int b) {
         if (trace)
@@ -3300,7 +3419,15 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     all_pinned &= pin_scale;
     if (!all_pinned && (rc = ensure_pinned(h, n))) return rc;
     if (!h->s_copy) HIPCHK(hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking));
-    if (!h->s_up) HIPCHK(hipStreamCreateWithFlags(&h->s_up, hipStreamNonBlocking));
+    if (!h->s_up) {
+        const char *upv = getenv("FARMS_UP_PRIO");  // A/B aid: hi | lo = the upload stream's priority
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (upv && (upv[0] == 'h' || upv[0] == 'l'))
+            HIPCHK(hipStreamCreateWithPriority(&h->s_up, hipStreamNonBlocking, upv[0] == 'h' ? hi : lo));
+        else
+            HIPCHK(hipStreamCreateWithFlags(&h->s_up, hipStreamNonBlocking));
+    }
     const int T = host_threads();
     // pinned staging: inputs x | y | t | p, records: six double columns, then scale
     int32_t *stg_in[4];
@@ -3369,6 +3496,76 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         return code ? code : rs;
     };
     int64_t S_all = 0;  // super-chunks of the call so far
+    // Record downloads of a sub-batch's super-chunks, enqueued on the copy
+    // stream only after the NEXT sub-batch's upload: with GPU_MAX_HW_QUEUES=4
+    // the upload and copy streams share one hardware queue, and an upload queued
+    // behind downloads that wait for pooling would hold the next sub-batch's
+    // fits until this one's pooling is done.
+    struct Download { int64_t S, a0; int p0, p1; hipEvent_t done; };
+    std::vector<Download> dl;
+    // downloads: k_export (default) or the runtime's copies (FARMS_D2H=copy, A/B aid)
+    const char *d2v = getenv("FARMS_D2H");
+    const bool d2h_kernel = !(d2v && std::strcmp(d2v, "copy") == 0);
+    const char *ddv = getenv("FARMS_DL_DEFER");  // A/B aid: 0 = downloads enqueued as each super-chunk is
+    const bool defer_dl = !(ddv && ddv[0] == '0');
+    const char *ntv = getenv("FARMS_EXPORT_NT");  // A/B aid: 1 = nontemporal stores in k_export
+    const bool export_nt = ntv && ntv[0] == '1';
+    const char *xwv = getenv("FARMS_EXPORT_WGS");
+    const int export_wgs = xwv ? std::max(1, std::min(4096, atoi(xwv))) : 128;
+    double *xdst[6];
+    int32_t *xdsti[5];
+    for (int c = 0; c < 6; ++c) xdst[c] = device_view(dst_col[c]);
+    xdsti[0] = device_view(dst_scale);
+    for (int c = 0; c < 4; ++c) xdsti[1 + c] = pin_echo[c] ? device_view(uecho[c]) : nullptr;
+    auto flush_downloads = [&]() -> int {
+        hipStream_t sd = h->s_copy;
+        for (const Download &q : dl) {
+            if ((int64_t)h->copy_ev.size() <= q.S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
+            ENQ(14, HIPCHK(hipStreamWaitEvent(sd, q.done, 0)));
+            const size_t k = (size_t)(q.p1 - q.p0);
+            const int64_t g0 = q.a0 + q.p0;
+            int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
+            if (d2h_kernel) {
+                ExportCols e{};
+                uintptr_t align = 0;
+                for (int c = 0; c < 6; ++c) {
+                    e.src[c] = h->io_rec[c] + g0;
+                    e.dst[c] = xdst[c] + g0;
+                    align |= (uintptr_t)e.src[c] | (uintptr_t)e.dst[c];
+                }
+                e.srci[0] = h->io_scale + g0;
+                e.dsti[0] = xdsti[0] + g0;
+                for (int c = 0; c < 4; ++c) {  // the x, y, t, p echo (vFlow.cpp:370-373) from the device copies
+                    e.srci[1 + c] = io_in[c] + g0;
+                    e.dsti[1 + c] = xdsti[1 + c] ? xdsti[1 + c] + g0 : nullptr;
+                }
+                for (int c = 0; c < 5; ++c)
+                    if (e.dsti[c]) align |= (uintptr_t)e.srci[c] | (uintptr_t)e.dsti[c];
+                e.n = (int64_t)k;
+                e.vec = (align & 15) == 0 ? (export_nt ? 2 : 1) : 0;
+                ENQ(15, hipLaunchKernelGGL(k_export, dim3(export_wgs), dim3(256), 0, sd, e));
+            } else {
+                for (int c = 0; c < 6; ++c)
+                    ENQ(15, HIPCHK(hipMemcpyAsync(dst_col[c] + g0, h->io_rec[c] + g0, 8 * k, hipMemcpyDeviceToHost, sd)));
+                HIPCHK(hipMemcpyAsync(dst_scale + g0, h->io_scale + g0, 4 * k, hipMemcpyDeviceToHost, sd));
+                // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
+                for (int c = 0; c < 4; ++c)
+                    if (pin_echo[c])
+                        HIPCHK(hipMemcpyAsync(uecho[c] + g0, io_in[c] + g0, 4 * k, hipMemcpyDeviceToHost, sd));
+            }
+            ENQ(16, HIPCHK(hipEventRecord(h->copy_ev[q.S], sd)));
+            enqueue_trace("download", q.S, 0);
+            if (any_host_copy) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    ready.push_back(Ready{q.S, g0, q.a0 + q.p1});
+                }
+                cv.notify_one();
+            }
+        }
+        dl.clear();
+        return FARMS_OK;
+    };
     // asynchronous sub-batches unless the call is profiled (timing and counters
     // are read back per call)
     const bool async = !h->profiling && !h->counting;
@@ -3401,34 +3598,17 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             rc = fail(FARMS_EHIP, "farms_process: host-to-device copy");
             break;
         }
+        tr("uploaded", b);
+        if ((rc = flush_downloads())) break;  // the previous sub-batch's, behind this upload
+        tr("downloads enqueued", b - 1);
         // ---- compute, with the record downloads hooked onto each super-chunk
         farms_records d{};
         d.r_true = h->io_rec[0] + a0; d.theta_true = h->io_rec[1] + a0; d.vx = h->io_rec[2] + a0;
         d.vy = h->io_rec[3] + a0; d.r_local = h->io_rec[4] + a0; d.theta_local = h->io_rec[5] + a0;
         d.scale = h->io_scale + a0;
-        double *const dcol[6] = {d.r_true, d.theta_true, d.vx, d.vy, d.r_local, d.theta_local};
         super_hook hook = [&](int, int p0, int p1, hipEvent_t done) -> int {
-            const int64_t S = S_all++;
-            if ((int64_t)h->copy_ev.size() <= S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
-            hipStream_t sd = h->s_copy;
-            HIPCHK(hipStreamWaitEvent(sd, done, 0));
-            const size_t k = (size_t)(p1 - p0);
-            const int64_t g0 = a0 + p0;
-            for (int c = 0; c < 6; ++c)
-                HIPCHK(hipMemcpyAsync(dst_col[c] + g0, dcol[c] + p0, 8 * k, hipMemcpyDeviceToHost, sd));
-            HIPCHK(hipMemcpyAsync(dst_scale + g0, d.scale + p0, 4 * k, hipMemcpyDeviceToHost, sd));
-            // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
-            for (int c = 0; c < 4; ++c)
-                if (pin_echo[c]) HIPCHK(hipMemcpyAsync(uecho[c] + g0, dev_in[c] + p0, 4 * k, hipMemcpyDeviceToHost, sd));
-            HIPCHK(hipEventRecord(h->copy_ev[S], sd));
-            if (any_host_copy) {
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    ready.push_back(Ready{S, g0, a0 + p1});
-                }
-                cv.notify_one();
-            }
-            return FARMS_OK;
+            dl.push_back(Download{S_all++, a0, p0, p1, done});  // enqueued after the next sub-batch's upload
+            return defer_dl ? FARMS_OK : flush_downloads();
         };
         rc = run_core(h, w, dev_in[0], dev_in[1], reinterpret_cast<const uint32_t *>(dev_in[2]), dev_in[3], m, &d,
                       &hook, 0, async, /*validated=*/true);
@@ -3437,6 +3617,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         pool_launches += h->stats.pool_launches;
         tr("enqueued", b);
     }
+    if (!rc) rc = flush_downloads();  // the last sub-batch's
     if (trace) {  // when the device finished each stream's work
         (void)hipStreamSynchronize(h->stream); tr("F done", nbat);
         (void)hipStreamSynchronize(h->s_pool); tr("P done", nbat);
@@ -3444,6 +3625,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     }
     rc = finish(rc);
     tr("copy-out done", nbat);
+    enq_report();
     if (rc) return rc;
     if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
     h->stats.n_events = n;

@@ -41,6 +41,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <new>
@@ -2239,6 +2240,7 @@ struct Work {
     std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
     hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
     hipEvent_t ready = nullptr;                // two-phase calls: the fits and the imported flows are in place
+    hipEvent_t fend = nullptr;                 // asynchronous calls: stream F's last work of the call
     bool busy = false;                         // `done` recorded and the set not yet reused
 };
 
@@ -2307,9 +2309,10 @@ struct farms_handle {
     double *io_rec[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     int32_t *io_scale = nullptr;
     int64_t io_cap = 0;
-    hipStream_t s_copy = nullptr, s_up = nullptr;
+    hipStream_t s_copy = nullptr;  // farms_process's uploads and record downloads (one stream: -3 ms at C3)
     std::vector<hipEvent_t> copy_ev;
-    hipEvent_t up_ev[2] = {};
+    std::vector<hipEvent_t> final_ev;  // per super-chunk of a farms_process call: its records are final
+    std::vector<hipEvent_t> up_ev;  // per sub-batch of a farms_process call: its upload landed
 };
 
 namespace {
@@ -2344,7 +2347,7 @@ int end_bit_for(int64_t WH) {
 
 // Every stream of the handle idle (nothing of an asynchronous call in flight).
 int sync_all(farms_handle *h) {
-    for (hipStream_t s : {h->stream, h->s_chain, h->s_pool, h->s_copy, h->s_up})
+    for (hipStream_t s : {h->stream, h->s_chain, h->s_pool, h->s_copy})
         if (s) HIPCHK(hipStreamSynchronize(s));
     for (Work &w : h->ws) w.busy = false;
     return FARMS_OK;
@@ -2487,52 +2490,9 @@ int ensure_sync_events(Work &w, size_t count) {
 // flow snapshots and cursors, P), the candidate ring continues by chunk number,
 // and `validated` skips the device-side range check (and its host sync).
 typedef std::function<int(int S, int p0, int p1, hipEvent_t done)> super_hook;
-// FARMS_HOST_TRACE=2: host timestamps of run_core's enqueue steps on stderr (diagnostic)
-// FARMS_HOST_TRACE=3: per-callsite host time of the enqueue calls (diagnostic)
-static const char *const kEnqSite[] = {"fit launch", "prep launch", "record ev_fit", "C wait gpool", "C wait ev_fit",
-                                       "k_flow launch", "k_chain launch", "k_pool_desc launch", "record ev_cand",
-                                       "P wait ev_cand", "k_pool launch", "k_true_polar launch", "record ev_pool",
-                                       "record gpool", "D2H wait", "D2H memcpy", "D2H record"};
-static double g_enq_us[17];
-static long g_enq_n[17];
-static bool enq_prof() {
-    static const char *v = getenv("FARMS_HOST_TRACE");
-    return v && v[0] == '3';
-}
-static void enq_report() {
-    if (!enq_prof()) return;
-    for (int i = 0; i < 17; ++i)
-        if (g_enq_n[i])
-            std::fprintf(stderr, "[farms enq] %-22s %7ld calls %10.1f us total %8.2f us/call\n", kEnqSite[i], g_enq_n[i],
-                         g_enq_us[i], g_enq_us[i] / g_enq_n[i]);
-    std::memset(g_enq_us, 0, sizeof(g_enq_us));
-    std::memset(g_enq_n, 0, sizeof(g_enq_n));
-}
-#define ENQ(id, stmt)                                                                                            \
-    do {                                                                                                        \
-        if (enq_prof()) {                                                                                       \
-            const auto enq_t0 = std::chrono::steady_clock::now();                                               \
-            stmt;                                                                                               \
-            g_enq_us[id] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - enq_t0).count(); \
-            ++g_enq_n[id];                                                                                      \
-        } else {                                                                                                \
-            stmt;                                                                                               \
-        }                                                                                                       \
-    } while (0)
-static void enqueue_trace(const char *what, int64_t a, int64_t b) {
-    static const char *v = getenv("FARMS_HOST_TRACE");
-    if (!v || v[0] != '2') return;
-    static const auto t0 = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[farms enq] %9.3f ms %s %lld %lld\n",
-                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), what,
-                 (long long)a, (long long)b);
-}
-int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
-             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0,
-             bool async = false, bool validated = false) {
-    const int n = (int)n64;
-    hipStream_t s = h->stream;
-    h->fresh = false;
+// The kernels' view of one call on workspace set w.
+Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
+             int n, farms_records *dout, bool async) {
     Ctx c{};
     c.W = h->W; c.H = h->H; c.n = n; c.WH = h->WH; c.WHs = (int64_t)h->W * h->H;
     c.X0 = h->X0; c.XR1 = h->X0 + h->WR; c.own_lo = h->own_lo; c.own_hi = h->own_hi;
@@ -2562,10 +2522,15 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.counters = h->counters;
     c.dbg_tc = h->counting && !async ? w.dbg_tc : nullptr;
 
-    const bool prof = h->profiling && !async;
+    return c;
+}
+
+// Before a call writes workspace set w: wait for the set's previous
+// asynchronous call, size its dependency events (and the profiling events).
+int claim_set(farms_handle *h, Work &w, int n, bool prof) {
+    hipStream_t s = h->stream;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
-    const int B = h->pool_batch;
-    const int n_super = ceil_div(n_pool_chunks, B);
+    const int n_super = ceil_div(n_pool_chunks, h->pool_batch);
     if (w.busy) {  // the set's previous (asynchronous) call is done with it before anything writes it
         HIPCHK(hipStreamWaitEvent(s, w.done, 0));
         w.busy = false;
@@ -2575,22 +2540,18 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (rc) return rc;
         HIPCHK(hipEventRecord(h->ev[0], s));
     }
-    // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
-    // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
-    {
-        int rc = ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
-        if (rc) return rc;
-    }
-    hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
-    auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
-    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
-    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
+    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
+}
 
-    // ---- prep (stream F): validate, pixel ids, sort by pixel, links, work order
-    if (phase == 2) {  // prepared by phase 1: its fits and the imported flows are in place at w.ready
-        if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
-        ev_prep = w.ready;
-    } else {
+// The prep of a call on set w (stream F): validate, pixel ids, sort by pixel,
+// links, fit descriptors, work order; records w.sync_ev[0].
+int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, bool prof) {
+    int rc = claim_set(h, w, n, prof);
+    if (rc) return rc;
+    hipStream_t s = h->stream;
+    const int n_pool_chunks = ceil_div(n, h->pool_chunk);
+    const uint32_t *dt = c.t;
+    hipEvent_t ev_prep = w.sync_ev[0];
     if (!validated) HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err,
                        h->pool_chunk, h->tile_bits, h->tile_shift);
@@ -2620,9 +2581,35 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     HIPCHK(hipEventRecord(ev_prep, s));
     if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
-    enqueue_trace("prep", h->super_base, n);
-    }  // prep
+    return FARMS_OK;
+}
 
+int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
+             int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0,
+             bool async = false, bool validated = false) {
+    const int n = (int)n64;
+    hipStream_t s = h->stream;
+    h->fresh = false;
+    Ctx c = make_ctx(h, w, dx, dy, dt, dp, n, dout, async);
+
+    const bool prof = h->profiling && !async;
+    const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
+    const int B = h->pool_batch;
+    const int n_super = ceil_div(n_pool_chunks, B);
+    {
+        int rc = phase == 2 ? claim_set(h, w, n, prof) : enqueue_prep(h, w, c, n, validated, prof);
+        if (rc) return rc;
+    }
+    // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
+    // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
+    hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
+    auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
+    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
+    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
+    if (phase == 2) {  // prepared by phase 1: its fits and the imported flows are in place at w.ready
+        if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
+        ev_prep = w.ready;
+    }
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
     //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
@@ -2670,14 +2657,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f], s));
         bool merged = false;
         if (fast_fit) {
-            ENQ(0, merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next));
+            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, w.Q + c0,
                                c1 - c0);
         }
-        if (!merged && next.blocks > 0) ENQ(1, launch_prep(next));
+        if (!merged && next.blocks > 0) launch_prep(next);
         if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
-        ENQ(2, HIPCHK(hipEventRecord(ev_fit(f), s)));
+        HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
             FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
@@ -2716,41 +2703,37 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         // keep the fit sweep one super-chunk ahead of the chain
         const int need = std::min(n_fit_chunks, ceil_div(std::min<int64_t>((int64_t)(ch1 + B) * h->pool_chunk, n),
                                                          h->fit_chunk));
-        enqueue_trace("super", Sg, fit_enqueued);
         while (fit_enqueued < need) {
             int rc = enqueue_fit(fit_enqueued++);
             if (rc) return rc;
         }
-        enqueue_trace("fits", Sg, fit_enqueued);
         // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
-        if (Sg >= 2) ENQ(3, HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0)));
+        if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
         {  // the chain reads the local flows of every event of the super-chunk
             const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
             const int fl = std::min(f, n_fit_chunks - 1);
-            if (fl > fit_waited) { ENQ(4, HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0))); fit_waited = fl; }
+            if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
         if (phase != 2) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-            ENQ(5, hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1));
+            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
         for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
-            ENQ(6, hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1)));
+            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1));
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-            ENQ(7, hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1));
+            hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
-        ENQ(8, HIPCHK(hipEventRecord(ev_cand(S), sc)));
-        enqueue_trace("chain", Sg, 0);
-        ENQ(9, HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0)));
+        HIPCHK(hipEventRecord(ev_cand(S), sc));
+        HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
-        ENQ(10, pl(c, p0, p1, sp));
+        pl(c, p0, p1, sp);
         if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
-        ENQ(11, hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1));
-        ENQ(12, HIPCHK(hipEventRecord(ev_pool(S), sp)));
-        ENQ(13, HIPCHK(hipEventRecord(h->gpool[Sg % 3], sp)));
-        enqueue_trace("pool", Sg, 0);
+        hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
+        HIPCHK(hipEventRecord(ev_pool(S), sp));
+        HIPCHK(hipEventRecord(h->gpool[Sg % 3], sp));
         if (on_super) {
             int rc = (*on_super)(S, p0, p1, ev_pool(S));
             if (rc) return rc;
@@ -2770,8 +2753,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         // chain's last step) and F's last work of the call (phase 2 has none):
         // the next call's fits on F do not wait for this call's pooling
         if (phase != 2) {
-            HIPCHK(hipEventRecord(ev_prep, s));  // (reused: F's end of this call)
-            HIPCHK(hipStreamWaitEvent(sp, ev_prep, 0));
+            HIPCHK(hipEventRecord(w.fend, s));
+            HIPCHK(hipStreamWaitEvent(sp, w.fend, 0));
         }
         HIPCHK(hipEventRecord(w.done, sp));
         w.busy = true;
@@ -2943,19 +2926,24 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // the fit sweep and the candidate chain are the latency-critical dependency
     // path: high priority; the bulk pooling launches fill the remaining CUs
     // (measured and rejected: a CU mask keeping pooling waves off some CUs of
-    // each XCD, other priority assignments: DESIGN.md §8)
+    // each XCD, other priority assignments: DESIGN.md §8).  The copy stream of
+    // farms_process is created with them: the runtime maps streams onto
+    // GPU_MAX_HW_QUEUES (4) hardware queues, and a copy stream created later,
+    // after another library's stream took a queue, shared F's queue (host path
+    // 113 instead of 97 ms at C3).
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess)
+        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     for (auto &ev : h->ev)
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     {
-        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->up_ev[0],
-                                         &h->up_ev[1], &h->ws[0].done, &h->ws[1].done, &h->ws[0].ready,
-                                         &h->ws[1].ready};
+        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end,
+                                         &h->ws[0].done, &h->ws[1].done, &h->ws[0].ready,
+                                         &h->ws[1].ready, &h->ws[0].fend, &h->ws[1].fend};
         for (hipEvent_t *ev : evs)
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
                 return bail(fail(FARMS_EHIP, "hipEventCreate"));
@@ -2978,7 +2966,6 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     if (h->s_copy) (void)hipStreamSynchronize(h->s_copy);
-    if (h->s_up) (void)hipStreamSynchronize(h->s_up);
     dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
     for (Work &w : h->ws) {
         free_workspace(w);
@@ -2986,6 +2973,7 @@ extern "C" int farms_destroy(farms_handle *h) {
         for (auto &ev : w.sync_ev) (void)hipEventDestroy(ev);
         if (w.done) (void)hipEventDestroy(w.done);
         if (w.ready) (void)hipEventDestroy(w.ready);
+        if (w.fend) (void)hipEventDestroy(w.fend);
     }
     for (auto &ev : h->gpool)
         if (ev) (void)hipEventDestroy(ev);
@@ -2998,8 +2986,8 @@ extern "C" int farms_destroy(farms_handle *h) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->kev) (void)hipEventDestroy(ev);
     for (auto &ev : h->copy_ev) (void)hipEventDestroy(ev);
+    for (auto &ev : h->final_ev) (void)hipEventDestroy(ev);
     if (h->s_copy) (void)hipStreamDestroy(h->s_copy);
-    if (h->s_up) (void)hipStreamDestroy(h->s_up);
     if (h->pin_in) (void)hipHostFree(h->pin_in);
     if (h->pin_out) (void)hipHostFree(h->pin_out);
     dfree(h->io_x); dfree(h->io_y); dfree(h->io_t); dfree(h->io_p); dfree(h->io_scale);
@@ -3254,78 +3242,6 @@ int ensure_io(farms_handle *h, int64_t n) {
 
 // Host memory the DMA engines reach directly (hipHostMalloc'd or registered):
 // such arrays skip the pinned staging copy.
-// Record download of the host path as a kernel: device columns -> pinned host
-// memory (stores over PCIe).  The runtime's own device-to-host copies are
-// blit kernels too, but eleven per super-chunk, each of 256 512-thread
-// workgroups, and under direct dispatch they fell 95 ms behind the compute at
-// C3; one launch of a few workgroups per super-chunk keeps pace with it.
-struct ExportCols {
-    const double *src[6];
-    double *dst[6];
-    const int32_t *srci[5];  // scale, then the x, y, t, p echo
-    int32_t *dsti[5];        // (nullptr: not exported)
-    int64_t n;
-    int vec;                 // every pointer 16-B aligned: double2 / int4 moves (2: nontemporal doubles)
-};
-
-__global__ __launch_bounds__(256) void k_export(ExportCols e) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e.vec) {
-        const int64_t n2 = e.n / 2, n4 = e.n / 4;
-        for (int64_t i = t0; i < n2; i += stride) {
-            double2 v[6];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) v[c] = reinterpret_cast<const double2 *>(e.src[c])[i];
-            if (e.vec == 2) {
-#pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    __builtin_nontemporal_store(v[c].x, e.dst[c] + 2 * i);
-                    __builtin_nontemporal_store(v[c].y, e.dst[c] + 2 * i + 1);
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 6; ++c) reinterpret_cast<double2 *>(e.dst[c])[i] = v[c];
-            }
-        }
-        for (int64_t i = t0; i < n4; i += stride) {
-#pragma unroll
-            for (int c = 0; c < 5; ++c)
-                if (e.dsti[c]) reinterpret_cast<int4 *>(e.dsti[c])[i] = reinterpret_cast<const int4 *>(e.srci[c])[i];
-        }
-        if (t0 == 0) {  // tails
-            for (int64_t i = 2 * n2; i < e.n; ++i)
-                for (int c = 0; c < 6; ++c) e.dst[c][i] = e.src[c][i];
-            for (int64_t i = 4 * n4; i < e.n; ++i)
-                for (int c = 0; c < 5; ++c)
-                    if (e.dsti[c]) e.dsti[c][i] = e.srci[c][i];
-        }
-        return;
-    }
-    for (int64_t i = t0; i < e.n; i += stride) {
-        double v[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) v[c] = e.src[c][i];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) e.dst[c][i] = v[c];
-#pragma unroll
-        for (int c = 0; c < 5; ++c)
-            if (e.dsti[c]) e.dsti[c][i] = e.srci[c][i];
-    }
-}
-
-// the device address of pinned host memory (that of a hipHostRegister-ed
-// range may differ from its host address)
-template <class T>
-T *device_view(T *p) {
-    hipPointerAttribute_t a{};
-    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return p;
-    }
-    return a.devicePointer ? static_cast<T *>(a.devicePointer) : p;
-}
-
 bool is_pinned(const void *p) {
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -3354,21 +3270,23 @@ void host_parallel(int64_t n, int T, Fn &&fn) {
 // pipelined in sub-batches of whole pooling super-chunks (about an eighth of
 // a long call each; consecutive calls are bitwise one call):
 //   upload: sub-batch b's events are range-checked and (pageable arrays)
-//     copied into pinned staging by host threads, then DMAed on the upload
-//     stream into workspace set b % 2 -- while the GPU still computes
-//     sub-batch b - 1 (run_core enqueues asynchronously);
-//   compute: run_core on set b % 2, chained on the streams behind b - 1;
+//     copied into pinned staging by host threads, then DMAed on the copy
+//     stream into the call's device copies -- while the GPU still computes
+//     sub-batch b - 1 (run_core enqueues asynchronously); pinned inputs are
+//     checked and uploaded for every sub-batch up front;
+//   compute: run_core on workspace set b % 2, chained on the streams behind
+//     b - 1;
 //   download: as each pooling super-chunk's records become final on the
-//     device (run_core's hook; enqueued behind the next sub-batch's upload,
-//     since the two copy streams may share a hardware queue) its columns are
-//     DMAed -- straight into the
-//     caller's arrays when they are pinned (with the x, y, t, p echo from the
-//     device copies), else into pinned staging, moved to the caller's arrays
-//     (with the echo) by host threads as each DMA lands.
+//     device (run_core's hook records an event), a host thread waits for it
+//     and enqueues the copies of its columns -- straight into the caller's
+//     arrays when they are pinned (with the x, y, t, p echo from the device
+//     copies), else into pinned staging, moved to the caller's arrays (with
+//     the echo) by host threads as each copy lands.
 // Only the first sub-batch's upload and the last super-chunk's download are
 // not hidden by compute.  An event outside the sensor stops the call with
-// FARMS_EINVAL before its sub-batch is enqueued (earlier sub-batches of a long
-// call have then been processed: reset the handle to start over).
+// FARMS_EINVAL before its sub-batch is enqueued (pinned inputs are checked and
+// uploaded up front, so nothing has run; otherwise earlier sub-batches of a
+// long call have been processed: reset the handle to start over).
 extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
@@ -3386,7 +3304,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     const char *sbv = getenv("FARMS_SUBBATCHES");  // A/B aid: 1 = one call, k = about n / k per sub-batch
     const int64_t nsub = sbv ? std::max(1, atoi(sbv)) : 8;
     const char *trv = getenv("FARMS_HOST_TRACE");   // 1: host timestamps of the pipeline on stderr
-    const bool trace = trv && (trv[0] >= '1' && trv[0] <= '3');
+    const bool trace = trv && (trv[0] == '1');
     const auto tr0 = std::chrono::steady_clock::now();
     auto tr = [&](const char *what, int b) {
         if (trace)
@@ -3399,8 +3317,8 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         if (n > 2 * per) sub = per;
     }
     const int nbat = ceil_div(n, sub);
-    int rc = ensure_capacity(h, h->ws[0], sub);
-    if (!rc && nbat > 1) rc = ensure_capacity(h, h->ws[1], sub);
+    int rc = FARMS_OK;
+    for (int k = 0; k < std::min(nbat, 2) && !rc; ++k) rc = ensure_capacity(h, h->ws[k], sub);  // set b % 2
     if (!rc) rc = ensure_io(h, n);
     if (rc) return rc;
     // per array: pinned host memory is DMAed directly, pageable memory goes
@@ -3409,6 +3327,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     bool pin_in[4], pin_col[6], pin_echo[4];
     bool all_pinned = true;
     for (int k = 0; k < 4; ++k) all_pinned &= (pin_in[k] = is_pinned(uin[k]));
+    const bool all_in_pinned = all_pinned;
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
     int32_t *const uecho[4] = {out->x, out->y, out->t, out->p};
     for (int k = 0; k < 6; ++k) all_pinned &= (pin_col[k] = is_pinned(ucol[k]));
@@ -3418,16 +3337,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     const bool pin_scale = is_pinned(out->scale);
     all_pinned &= pin_scale;
     if (!all_pinned && (rc = ensure_pinned(h, n))) return rc;
-    if (!h->s_copy) HIPCHK(hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking));
-    if (!h->s_up) {
-        const char *upv = getenv("FARMS_UP_PRIO");  // A/B aid: hi | lo = the upload stream's priority
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (upv && (upv[0] == 'h' || upv[0] == 'l'))
-            HIPCHK(hipStreamCreateWithPriority(&h->s_up, hipStreamNonBlocking, upv[0] == 'h' ? hi : lo));
-        else
-            HIPCHK(hipStreamCreateWithFlags(&h->s_up, hipStreamNonBlocking));
-    }
+
     const int T = host_threads();
     // pinned staging: inputs x | y | t | p, records: six double columns, then scale
     int32_t *stg_in[4];
@@ -3453,6 +3363,11 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             hipEvent_t ev;
             HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             h->copy_ev.push_back(ev);
+        }
+        while ((int64_t)h->final_ev.size() < n_super_all) {
+            hipEvent_t ev;
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            h->final_ev.push_back(ev);
         }
     }
     struct Ready { int64_t S, p0, p1; };
@@ -3496,84 +3411,77 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         return code ? code : rs;
     };
     int64_t S_all = 0;  // super-chunks of the call so far
-    // Record downloads of a sub-batch's super-chunks, enqueued on the copy
-    // stream only after the NEXT sub-batch's upload: with GPU_MAX_HW_QUEUES=4
-    // the upload and copy streams share one hardware queue, and an upload queued
-    // behind downloads that wait for pooling would hold the next sub-batch's
-    // fits until this one's pooling is done.
+    // Record downloads: a host thread enqueues each super-chunk's copies on the
+    // copy stream once its records are final (their event has completed), so
+    // the copy queue never holds a wait on the pooling.  Measured (C3, pinned,
+    // FARMS_HOST_TRACE=1): with the waits enqueued in the copy queue the copies
+    // fell 47-95 ms behind the pooling (more the earlier they were enqueued),
+    // although the host enqueued everything within 10 ms; enqueued only when
+    // ready they finish within 1 ms of the last pooling launch.
     struct Download { int64_t S, a0; int p0, p1; hipEvent_t done; };
-    std::vector<Download> dl;
-    // downloads: k_export (default) or the runtime's copies (FARMS_D2H=copy, A/B aid)
-    const char *d2v = getenv("FARMS_D2H");
-    const bool d2h_kernel = !(d2v && std::strcmp(d2v, "copy") == 0);
-    const char *ddv = getenv("FARMS_DL_DEFER");  // A/B aid: 0 = downloads enqueued as each super-chunk is
-    const bool defer_dl = !(ddv && ddv[0] == '0');
-    const char *ntv = getenv("FARMS_EXPORT_NT");  // A/B aid: 1 = nontemporal stores in k_export
-    const bool export_nt = ntv && ntv[0] == '1';
-    const char *xwv = getenv("FARMS_EXPORT_WGS");
-    const int export_wgs = xwv ? std::max(1, std::min(4096, atoi(xwv))) : 128;
-    double *xdst[6];
-    int32_t *xdsti[5];
-    for (int c = 0; c < 6; ++c) xdst[c] = device_view(dst_col[c]);
-    xdsti[0] = device_view(dst_scale);
-    for (int c = 0; c < 4; ++c) xdsti[1 + c] = pin_echo[c] ? device_view(uecho[c]) : nullptr;
-    auto flush_downloads = [&]() -> int {
+    auto enqueue_download = [&](const Download &q) -> int {
         hipStream_t sd = h->s_copy;
-        for (const Download &q : dl) {
-            if ((int64_t)h->copy_ev.size() <= q.S) return fail(FARMS_EHIP, "farms_process: super-chunk count");
-            ENQ(14, HIPCHK(hipStreamWaitEvent(sd, q.done, 0)));
-            const size_t k = (size_t)(q.p1 - q.p0);
-            const int64_t g0 = q.a0 + q.p0;
-            int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
-            if (d2h_kernel) {
-                ExportCols e{};
-                uintptr_t align = 0;
-                for (int c = 0; c < 6; ++c) {
-                    e.src[c] = h->io_rec[c] + g0;
-                    e.dst[c] = xdst[c] + g0;
-                    align |= (uintptr_t)e.src[c] | (uintptr_t)e.dst[c];
-                }
-                e.srci[0] = h->io_scale + g0;
-                e.dsti[0] = xdsti[0] + g0;
-                for (int c = 0; c < 4; ++c) {  // the x, y, t, p echo (vFlow.cpp:370-373) from the device copies
-                    e.srci[1 + c] = io_in[c] + g0;
-                    e.dsti[1 + c] = xdsti[1 + c] ? xdsti[1 + c] + g0 : nullptr;
-                }
-                for (int c = 0; c < 5; ++c)
-                    if (e.dsti[c]) align |= (uintptr_t)e.srci[c] | (uintptr_t)e.dsti[c];
-                e.n = (int64_t)k;
-                e.vec = (align & 15) == 0 ? (export_nt ? 2 : 1) : 0;
-                ENQ(15, hipLaunchKernelGGL(k_export, dim3(export_wgs), dim3(256), 0, sd, e));
-            } else {
-                for (int c = 0; c < 6; ++c)
-                    ENQ(15, HIPCHK(hipMemcpyAsync(dst_col[c] + g0, h->io_rec[c] + g0, 8 * k, hipMemcpyDeviceToHost, sd)));
-                HIPCHK(hipMemcpyAsync(dst_scale + g0, h->io_scale + g0, 4 * k, hipMemcpyDeviceToHost, sd));
-                // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
-                for (int c = 0; c < 4; ++c)
-                    if (pin_echo[c])
-                        HIPCHK(hipMemcpyAsync(uecho[c] + g0, io_in[c] + g0, 4 * k, hipMemcpyDeviceToHost, sd));
+        const size_t k = (size_t)(q.p1 - q.p0);
+        const int64_t g0 = q.a0 + q.p0;
+        for (int c = 0; c < 6; ++c)
+            HIPCHK(hipMemcpyAsync(dst_col[c] + g0, h->io_rec[c] + g0, 8 * k, hipMemcpyDeviceToHost, sd));
+        HIPCHK(hipMemcpyAsync(dst_scale + g0, h->io_scale + g0, 4 * k, hipMemcpyDeviceToHost, sd));
+        // the x, y, t, p echo (vFlow.cpp:370-373) of pinned columns from the device copies
+        int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
+        for (int c = 0; c < 4; ++c)
+            if (pin_echo[c]) HIPCHK(hipMemcpyAsync(uecho[c] + g0, io_in[c] + g0, 4 * k, hipMemcpyDeviceToHost, sd));
+        HIPCHK(hipEventRecord(h->copy_ev[q.S], sd));
+        if (any_host_copy) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                ready.push_back(Ready{q.S, g0, q.a0 + q.p1});
             }
-            ENQ(16, HIPCHK(hipEventRecord(h->copy_ev[q.S], sd)));
-            enqueue_trace("download", q.S, 0);
-            if (any_host_copy) {
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    ready.push_back(Ready{q.S, g0, q.a0 + q.p1});
-                }
-                cv.notify_one();
-            }
+            cv.notify_one();
         }
-        dl.clear();
         return FARMS_OK;
+    };
+    std::mutex dmu;
+    std::condition_variable dcv;
+    std::deque<Download> dq;
+    bool dclosed = false;
+    std::atomic<int> dl_rc{0};
+    std::thread dlt([&]() {
+        if (hipSetDevice(h->prm.device) != hipSuccess) dl_rc = FARMS_EHIP;
+        for (;;) {
+            Download q;
+            {
+                std::unique_lock<std::mutex> lk(dmu);
+                dcv.wait(lk, [&] { return !dq.empty() || dclosed; });
+                if (dq.empty()) return;
+                q = dq.front();
+                dq.pop_front();
+            }
+            if (dl_rc) continue;  // a failed download: drain the queue, the call reports it
+            if (hipEventSynchronize(q.done) != hipSuccess) { dl_rc = FARMS_EHIP; continue; }
+            if (int r = enqueue_download(q)) dl_rc = r;
+        }
+    });
+    auto close_downloads = [&]() {
+        {
+            std::lock_guard<std::mutex> lk(dmu);
+            dclosed = true;
+        }
+        dcv.notify_all();
+        dlt.join();
     };
     // asynchronous sub-batches unless the call is profiled (timing and counters
     // are read back per call)
     const bool async = !h->profiling && !h->counting;
     int fit_launches = 0, pool_launches = 0;
-    for (int b = 0; b < nbat && !rc; ++b) {
+    while ((int)h->up_ev.size() < nbat) {
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        h->up_ev.push_back(ev);
+    }
+    // range check (vFlow.cpp:264 indexes the surfaces unchecked), staging and
+    // upload of sub-batch b into the call's device copies (nothing to wait for)
+    auto upload = [&](int b) -> int {
         const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
-        Work &w = h->ws[b & 1];
-        // ---- range check (vFlow.cpp:264 indexes the surfaces unchecked) and staging
         std::atomic<int> oor{0};
         host_parallel(m, T, [&](int64_t i0, int64_t i1) {
             const int64_t e0 = a0 + i0, k = i1 - i0;
@@ -3585,30 +3493,52 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
                 if (!pin_in[c]) std::memcpy(stg_in[c] + e0, static_cast<const int32_t *>(uin[c]) + e0, 4 * k);
         });
         tr("staged", b);
-        if (oor) { rc = fail(FARMS_EINVAL, "event outside the width x height sensor"); break; }
-        // ---- upload (the call's device copies: nothing to wait for)
-        hipStream_t su = h->s_up;
-        int32_t *const dev_in[4] = {h->io_x + a0, h->io_y + a0, h->io_t + a0, h->io_p + a0};
-        if (hipMemcpyAsync(dev_in[0], src_in[0] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(dev_in[1], src_in[1] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(dev_in[2], src_in[2] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipMemcpyAsync(dev_in[3], src_in[3] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess ||
-            hipEventRecord(h->up_ev[b & 1], su) != hipSuccess ||
-            hipStreamWaitEvent(h->stream, h->up_ev[b & 1], 0) != hipSuccess) {
-            rc = fail(FARMS_EHIP, "farms_process: host-to-device copy");
-            break;
-        }
+        if (oor) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+        hipStream_t su = h->s_copy;
+        int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
+        for (int c = 0; c < 4; ++c)
+            if (hipMemcpyAsync(io_in[c] + a0, src_in[c] + a0, 4 * m, hipMemcpyHostToDevice, su) != hipSuccess)
+                return fail(FARMS_EHIP, "farms_process: host-to-device copy");
+        HIPCHK(hipEventRecord(h->up_ev[b], su));
         tr("uploaded", b);
-        if ((rc = flush_downloads())) break;  // the previous sub-batch's, behind this upload
-        tr("downloads enqueued", b - 1);
-        // ---- compute, with the record downloads hooked onto each super-chunk
+        return FARMS_OK;
+    };
+    // pinned inputs: every sub-batch's upload is enqueued up front (FARMS_UP_AHEAD=0:
+    // one ahead of the compute, as for staged inputs)
+    const char *uav = getenv("FARMS_UP_AHEAD");
+    const bool up_ahead = all_in_pinned && !(uav && uav[0] == '0');
+    auto records_of = [&](int64_t a0) {
         farms_records d{};
         d.r_true = h->io_rec[0] + a0; d.theta_true = h->io_rec[1] + a0; d.vx = h->io_rec[2] + a0;
         d.vy = h->io_rec[3] + a0; d.r_local = h->io_rec[4] + a0; d.theta_local = h->io_rec[5] + a0;
         d.scale = h->io_scale + a0;
-        super_hook hook = [&](int, int p0, int p1, hipEvent_t done) -> int {
-            dl.push_back(Download{S_all++, a0, p0, p1, done});  // enqueued after the next sub-batch's upload
-            return defer_dl ? FARMS_OK : flush_downloads();
+        return d;
+    };
+    int uploaded = 0;
+    for (int b = 0; b < nbat && !rc; ++b) {
+        const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
+        Work &w = h->ws[b & 1];
+        while (!rc && uploaded < (up_ahead ? nbat : b + 1)) rc = upload(uploaded++);
+        if (rc) break;
+        int32_t *const dev_in[4] = {h->io_x + a0, h->io_y + a0, h->io_t + a0, h->io_p + a0};
+        if (hipStreamWaitEvent(h->stream, h->up_ev[b], 0) != hipSuccess) {
+            rc = fail(FARMS_EHIP, "farms_process: upload wait");
+            break;
+        }
+        // ---- compute, with the record downloads hooked onto each super-chunk
+        farms_records d = records_of(a0);
+        super_hook hook = [&](int, int p0, int p1, hipEvent_t) -> int {
+            // an event of the call's own (the set's pooling events are recorded again by later sub-batches)
+            if ((int64_t)h->final_ev.size() <= S_all || (int64_t)h->copy_ev.size() <= S_all)
+                return fail(FARMS_EHIP, "farms_process: super-chunk count");
+            HIPCHK(hipEventRecord(h->final_ev[S_all], h->s_pool));
+            {
+                std::lock_guard<std::mutex> lk(dmu);
+                dq.push_back(Download{S_all, a0, p0, p1, h->final_ev[S_all]});
+            }
+            ++S_all;
+            dcv.notify_one();
+            return FARMS_OK;
         };
         rc = run_core(h, w, dev_in[0], dev_in[1], reinterpret_cast<const uint32_t *>(dev_in[2]), dev_in[3], m, &d,
                       &hook, 0, async, /*validated=*/true);
@@ -3617,15 +3547,15 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         pool_launches += h->stats.pool_launches;
         tr("enqueued", b);
     }
-    if (!rc) rc = flush_downloads();  // the last sub-batch's
     if (trace) {  // when the device finished each stream's work
         (void)hipStreamSynchronize(h->stream); tr("F done", nbat);
         (void)hipStreamSynchronize(h->s_pool); tr("P done", nbat);
-        (void)hipStreamSynchronize(h->s_copy); tr("D2H done", nbat);
     }
+    close_downloads();
+    if (!rc && dl_rc) rc = fail(dl_rc, "farms_process: record download");
+    if (trace) { (void)hipStreamSynchronize(h->s_copy); tr("D2H done", nbat); }
     rc = finish(rc);
     tr("copy-out done", nbat);
-    enq_report();
     if (rc) return rc;
     if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
     h->stats.n_events = n;

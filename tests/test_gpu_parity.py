@@ -334,16 +334,24 @@ def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
     assert g1.n == 777 and np.array_equal(g1.scale, dd["scale"][:777])
 
 
-def test_host_path_out_of_sensor_in_a_later_sub_batch():
-    """An event outside the sensor stops a pipelined call before its sub-batch;
-    after a reset the handle processes the stream as if fresh."""
+@pytest.mark.parametrize("pin", [False, True])
+def test_host_path_out_of_sensor_in_a_later_sub_batch(pin):
+    """An event outside the sensor stops a pipelined call before its sub-batch
+    (pinned inputs: before any, their uploads are all checked up front); after
+    a reset the handle processes the stream as if fresh."""
     ev = farms.synth_config(3, 2_000_000)
     x, y, t, p = ev.relative()
     xb = x.copy()
     xb[-5] = 1280
+    keep = []
+    ins = [xb, y, t, p]
+    if pin:
+        for i in range(4):
+            ins[i], own = farms.pinned(ins[i])
+            keep.append(own)
     with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
         with pytest.raises(farms.FarmsError) as ei:
-            fm.process(xb, y, t, p)
+            fm.process(*ins)
         assert ei.value.code == farms.FARMS_EINVAL
         fm.reset()
         a = fm.process(x, y, t, p)

@@ -3272,8 +3272,7 @@ void host_parallel(int64_t n, int T, Fn &&fn) {
 //   upload: sub-batch b's events are range-checked and (pageable arrays)
 //     copied into pinned staging by host threads, then DMAed on the copy
 //     stream into the call's device copies -- while the GPU still computes
-//     sub-batch b - 1 (run_core enqueues asynchronously); pinned inputs are
-//     checked and uploaded for every sub-batch up front;
+//     sub-batch b - 1 (run_core enqueues asynchronously);
 //   compute: run_core on workspace set b % 2, chained on the streams behind
 //     b - 1;
 //   download: as each pooling super-chunk's records become final on the
@@ -3284,9 +3283,8 @@ void host_parallel(int64_t n, int T, Fn &&fn) {
 //     the echo) by host threads as each copy lands.
 // Only the first sub-batch's upload and the last super-chunk's download are
 // not hidden by compute.  An event outside the sensor stops the call with
-// FARMS_EINVAL before its sub-batch is enqueued (pinned inputs are checked and
-// uploaded up front, so nothing has run; otherwise earlier sub-batches of a
-// long call have been processed: reset the handle to start over).
+// FARMS_EINVAL before its sub-batch is enqueued (earlier sub-batches of a long
+// call have then been processed: reset the handle to start over).
 extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y, const uint32_t *t,
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
@@ -3327,7 +3325,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     bool pin_in[4], pin_col[6], pin_echo[4];
     bool all_pinned = true;
     for (int k = 0; k < 4; ++k) all_pinned &= (pin_in[k] = is_pinned(uin[k]));
-    const bool all_in_pinned = all_pinned;
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
     int32_t *const uecho[4] = {out->x, out->y, out->t, out->p};
     for (int k = 0; k < 6; ++k) all_pinned &= (pin_col[k] = is_pinned(ucol[k]));
@@ -3503,10 +3500,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         tr("uploaded", b);
         return FARMS_OK;
     };
-    // pinned inputs: every sub-batch's upload is enqueued up front (FARMS_UP_AHEAD=0:
-    // one ahead of the compute, as for staged inputs)
-    const char *uav = getenv("FARMS_UP_AHEAD");
-    const bool up_ahead = all_in_pinned && !(uav && uav[0] == '0');
     auto records_of = [&](int64_t a0) {
         farms_records d{};
         d.r_true = h->io_rec[0] + a0; d.theta_true = h->io_rec[1] + a0; d.vx = h->io_rec[2] + a0;
@@ -3518,7 +3511,9 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     for (int b = 0; b < nbat && !rc; ++b) {
         const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
         Work &w = h->ws[b & 1];
-        while (!rc && uploaded < (up_ahead ? nbat : b + 1)) rc = upload(uploaded++);
+        // (pinned inputs uploaded all up front: 1.5 ms slower at C3, the burst of
+        // uploads slows the first sub-batches' kernels more)
+        while (!rc && uploaded < b + 1) rc = upload(uploaded++);
         if (rc) break;
         int32_t *const dev_in[4] = {h->io_x + a0, h->io_y + a0, h->io_t + a0, h->io_p + a0};
         if (hipStreamWaitEvent(h->stream, h->up_ev[b], 0) != hipSuccess) {

@@ -337,8 +337,8 @@ def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
 @pytest.mark.parametrize("pin", [False, True])
 def test_host_path_out_of_sensor_in_a_later_sub_batch(pin):
     """An event outside the sensor stops a pipelined call before its sub-batch
-    (pinned inputs: before any, their uploads are all checked up front); after
-    a reset the handle processes the stream as if fresh."""
+    (pinned or pageable inputs); after a reset the handle processes the stream
+    as if fresh."""
     ev = farms.synth_config(3, 2_000_000)
     x, y, t, p = ev.relative()
     xb = x.copy()

@@ -140,11 +140,12 @@ constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
 // valid while candidate slots stay below 2^24 (W * H <= kMaxSlots)
 constexpr int kRowBias = 1 << 14;  // flattened positions of a window < 128 x 128
 constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
-#ifndef FARMS_POOL_HALVES
-#define FARMS_POOL_HALVES 1  // candidates per lane per pooling step (1 or 2)
-#endif
-// k_pool staging: {L, L cos, L sin, 1} and k0 of the 64 x FARMS_POOL_HALVES entries of a step, 8-B words
-constexpr int kPoolValWords = (4 * 64 + 8) * FARMS_POOL_HALVES;
+// candidates per lane per pooling step (2, halving the scan's dependent round
+// trips, took 20 more VGPRs and one wave per SIMD: C3 550.9 against 573
+// Mevents/s, round 3)
+constexpr int kPoolHalves = 1;
+// k_pool staging: {L, L cos, L sin, 1} and k0 of the 64 x kPoolHalves entries of a step, 8-B words
+constexpr int kPoolValWords = (4 * 64 + 8) * kPoolHalves;
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -1868,7 +1869,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     // contributor count as a sum of 1.0: exact); lanes past 4K fold junk
     const int grp = lane / K < 3 ? lane / K : 3;
     const int kk = lane - grp * K;
-    constexpr int NH = FARMS_POOL_HALVES;  // candidates per lane per step: a step covers 64 * NH positions
+    constexpr int NH = kPoolHalves;  // candidates per lane per step: a step covers 64 * NH positions
 #pragma unroll
     for (int h = 0; h < NH; ++h) s_val[4 * (lane + 64 * h) + 3] = 1.0;  // the count's "value" (staging never overwrites it)
     const uint64_t lt = (1ull << lane) - 1;
@@ -2070,7 +2071,7 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     uint64_t *s_start = s_dyn;
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
-    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64 * FARMS_POOL_HALVES);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64 * kPoolHalves);
     const int w = c0 + work_block();
     if (w >= c1) return;
     // the event and its fields in one 16-B load (k_pool_desc)

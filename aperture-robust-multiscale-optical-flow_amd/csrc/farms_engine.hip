@@ -1461,7 +1461,11 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
     }
 }
 
-constexpr int kGroupCells = 256;  // cells per candidate group = one k_chain wavefront (4 bitmap words)
+// cells per candidate group = one k_chain wavefront (4 bitmap words).  Measured
+// at C3 (round 3): 128 cells (78 VGPRs, 6 waves; or 64 VGPRs, 8 waves) 92-95 ms
+// per step, 512 cells (229 VGPRs, 2 waves) 95 ms, against 87.5 for 256: more
+// chain waves take slots from the fit and pooling, fewer lengthen the chain.
+constexpr int kGroupCells = 256;
 
 
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling

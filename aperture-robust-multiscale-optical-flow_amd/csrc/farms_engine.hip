@@ -253,7 +253,10 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
 // Grouped variant: runs of 8 consecutive logical blocks stay on one XCD and
 // the runs go round-robin over the XCDs (locality without uneven shares).
 // Bijective on [0, G) when G is a multiple of 64; other grids keep blockIdx.
-constexpr int kFitRun = 8;  // consecutive fit blocks per XCD run
+// consecutive fit blocks per XCD run (round 3, C3: runs of 16, 32 and 128
+// blocks all within 0.3 ms of 8 per step; the L2 sharing of neighbouring
+// tiles does not pace the fit)
+constexpr int kFitRun = 8;
 __device__ __forceinline__ int xcd_block_grouped(int b, int G) {
     constexpr int R = kFitRun;
     if (G % (8 * R)) return b;

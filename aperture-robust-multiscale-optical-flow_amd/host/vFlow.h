@@ -64,6 +64,7 @@ public:
 private:
     long process(bool write_output);
     int ensure_handle();
+    void print_serial_timing(long us, const double *vx, const double *vy, int64_t n);
 
     bool DEBUGMODE = false;
     double numEvents = 0;

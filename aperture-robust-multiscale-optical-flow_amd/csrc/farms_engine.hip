@@ -288,6 +288,16 @@ __global__ void k_prep(Ctx c, uint32_t *pix, int32_t *iota, uint32_t *wkey, int 
     iota[e] = e;
 }
 
+// Range check of a call's events (device arrays), on the copy stream: the
+// host waits for it there instead of behind stream F's queue (where the prep of
+// a two-phase fit waits for the pooling that last used its workspace set).
+__global__ void k_validate(const int32_t *x, const int32_t *y, int n, int x0, int x1, int H, int *err) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int ex = x[e], ey = y[e];
+    if (ex < x0 || ex >= x1 || ey < 0 || ey >= H) atomicOr(err, 1);
+}
+
 // Per position k of P (events sorted by pixel, then index): PT[k] = {event,
 // stamp}, and the event's link record, one 16-B scatter per event.  The stamp
 // of the previous position comes from the neighbouring lane.
@@ -2227,7 +2237,10 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // Per-call workspace.  Two sets: the host-array path pipelines a call in
 // sub-batches, and sub-batch b + 1's upload and prep (set (b+1) % 2) run while
-// sub-batch b's sweeps still read set b % 2.
+// sub-batch b's sweeps still read set b % 2.  The two-phase strip calls
+// alternate too: the fit of sub-batch b+2 waits for the pooling of b (a third
+// set that let it run ahead measured slower: its fit waves crowd the pooling,
+// DESIGN.md §6).
 struct Work {
     int64_t cap = 0;
     uint32_t *pix = nullptr, *skey = nullptr;
@@ -2560,15 +2573,18 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     const int n_pool_chunks = ceil_div(n, h->pool_chunk);
     const uint32_t *dt = c.t;
     hipEvent_t ev_prep = w.sync_ev[0];
-    if (!validated) HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err,
-                       h->pool_chunk, h->tile_bits, h->tile_shift);
-    if (!validated) {
+    if (!validated) {  // on the copy stream (idle in device calls): no wait behind F
+        hipStream_t sv = h->s_copy;
         int herr = 0;
-        HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), sv));
+        hipLaunchKernelGGL(k_validate, dim3(ceil_div(n, 256)), dim3(256), 0, sv, c.x, c.y, n, c.X0, c.XR1, c.H, h->err);
+        HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, sv));
+        HIPCHK(hipStreamSynchronize(sv));
         if (herr) return fail(FARMS_EINVAL, "event outside the width x height sensor");
     }
+    // (k_prep's own flag goes to the second word: the events are in range here)
+    hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err + 1,
+                       h->pool_chunk, h->tile_bits, h->tile_shift);
     size_t bytes = w.cub_bytes;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, bytes, w.pix, w.skey, w.iota, w.P, n, 0,
                                               end_bit_for(h->WH), s));
@@ -2907,8 +2923,10 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         h->pool_batch = kDefaultPoolBatch / 2;
     }
     {  // smaller sensors pool fewer events per chunk: the default scales with the
-       // sensor's linear size (nearest power of two; 320x320: 2048, measured best)
-        const double target = h->pool_chunk * std::sqrt((double)h->W * h->H / (1280.0 * 720.0));
+       // linear size of the stored region (nearest power of two; 320x320: 2048,
+       // measured best; an x-strip of 4 or 8 on 1280x720: 4096, so that its
+       // chunks span a time closer to a whole-sensor chunk's)
+        const double target = h->pool_chunk * std::sqrt((double)h->WR * h->H / (1280.0 * 720.0));
         while (h->pool_chunk > 1024 && h->pool_chunk > target * std::sqrt(2.0)) h->pool_chunk /= 2;
     }
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
@@ -2950,19 +2968,23 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     {
         std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end,
-                                         &h->ws[0].done, &h->ws[1].done, &h->ws[0].ready,
-                                         &h->ws[1].ready, &h->ws[0].fend, &h->ws[1].fend};
+                                         };
+        for (Work &w : h->ws) {
+            evs.push_back(&w.done);
+            evs.push_back(&w.ready);
+            evs.push_back(&w.fend);
+        }
         for (hipEvent_t *ev : evs)
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
                 return bail(fail(FARMS_EHIP, "hipEventCreate"));
     }
     if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
-        (rc = dalloc(&h->fsnap, h->WH)) || (rc = dalloc(&h->ws[0].pcur, h->WH)) ||
-        (rc = dalloc(&h->ws[0].pend, h->WH)) || (rc = dalloc(&h->ws[1].pcur, h->WH)) ||
-        (rc = dalloc(&h->ws[1].pend, h->WH)) ||
+        (rc = dalloc(&h->fsnap, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
-        (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 1)) || (rc = dalloc(&h->counters, 8)))
+        (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 2)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
+    for (Work &w : h->ws)
+        if ((rc = dalloc(&w.pcur, h->WH)) || (rc = dalloc(&w.pend, h->WH))) return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
     return FARMS_OK;

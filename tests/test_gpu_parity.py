@@ -27,9 +27,19 @@ SENSOR = {1: (128, 128), 2: (320, 320), 3: (1280, 720)}
 def oracles(x, y, t, p, height, width, fs, inl=5, jump=5, maxw=50):
     """Records of the reference restatement (glibc libm) and of the same
     restatement with the HIP path's correctly rounded libm."""
-    r = OracleFlow(height, width, fs, inl, jump, maxw).process(x, y, t, p)
-    rc = OracleFlow(height, width, fs, inl, jump, maxw, libm="cr").process(x, y, t, p)
-    return r, rc
+    import threading
+
+    refs = {}
+
+    def run(libm):  # in parallel threads (ctypes releases the GIL)
+        refs[libm] = OracleFlow(height, width, fs, inl, jump, maxw, libm=libm).process(x, y, t, p)
+
+    th = [threading.Thread(target=run, args=(m,)) for m in ("glibc", "cr")]
+    for a in th:
+        a.start()
+    for a in th:
+        a.join()
+    return refs["glibc"], refs["cr"]
 
 
 def run_pair(ev, width, height, fs, inl=5, jump=5, maxw=50, **kw):
@@ -89,11 +99,12 @@ def test_config2_full_stream_vs_oracle():
 
 
 def test_config4_stream_vs_oracle():
-    """BASELINE config 4's own stream (seed 0x5EED0004, fs 7, 11 scales)."""
-    ev = farms.synth_config(4, 150_000)
+    """BASELINE config 4's own stream (seed 0x5EED0004, fs 7, 11 scales): a
+    500k-event head (the oracle takes ~12 s per libm)."""
+    ev = farms.synth_config(4, 500_000)
     g, r, rc = run_pair(ev, 1280, 720, 7)
     rep = assert_parity(g, r, 720, 1280, rc=rc)
-    assert rep["valid_ref"] > 150_000 // 20
+    assert rep["valid_ref"] > 500_000 // 20
 
 
 def test_short_wide_sensor_double_visits():
@@ -118,8 +129,8 @@ def test_short_wide_sensor_double_visits():
 
 
 def test_three_scales_vs_oracle():
-    """BASELINE config 5 shape: fs=7 with scales {0,25,50}."""
-    ev = farms.synth_config(5, 120_000)
+    """BASELINE config 5 shape: fs=7 with scales {0,25,50}, a 500k-event head."""
+    ev = farms.synth_config(5, 500_000)
     g, r, rc = run_pair(ev, 1280, 720, 7, jump=25, maxw=50)
     assert_parity(g, r, 720, 1280, 25, 50, rc=rc)
     assert set(np.unique(g.scale)) <= {0, 25, 50}

@@ -31,6 +31,14 @@ for S in $STAGES; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
       python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --host-steps 0 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
     rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log | cut -c1-300 ;;
+  ranksim)  # N=8 rank simulations (tools/strip_rank.py): strips ranks 0, 3, 7; segments rank 3
+    timeout -k 10 500 python3 -u tools/strip_rank.py --split strips --n 8 --ranks ${RANKS:-0,3,7} \
+      > gpurun_out/ranksim_strips_n8.log 2>&1
+    rc=$?; echo "ranksim strips rc=$rc"; tail -1 gpurun_out/ranksim_strips_n8.log
+    [ $rc -ne 0 ] && exit $rc
+    timeout -k 10 300 python3 -u tools/strip_rank.py --split segments --n 8 --ranks 3 \
+      > gpurun_out/ranksim_segments_n8.log 2>&1
+    rc=$?; echo "ranksim segments rc=$rc"; tail -1 gpurun_out/ranksim_segments_n8.log ;;
   *) echo "unknown stage $S"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && exit $rc

@@ -4,14 +4,11 @@
 cd /root/repo
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest tests/test_cli.py -m gpu -x -v --timeout 120 --timeout-method thread \
-  > gpurun_out/cli_gpu.log 2>&1 || { tail -30 gpurun_out/cli_gpu.log; exit 1; }
-tail -2 gpurun_out/cli_gpu.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/strip_prof -o strip -- \
   python3 -u tools/strip_rank.py --split strips --n 8 --ranks 3 --reps 1 ${SIM_ARGS:-} \
   > gpurun_out/strip_prof.log 2>&1 || exit $?
-tail -3 gpurun_out/strip_prof.log
-for P in ${POOLS:-0 2048 1024}; do
+tail -2 gpurun_out/strip_prof.log
+for P in ${POOLS:-0 4096 2048}; do
   timeout -k 10 300 python3 -u tools/strip_rank.py --split strips --n 8 --ranks 3 --pool $P ${SIM_ARGS:-} \
     > gpurun_out/strip_pool_$P.log 2>&1 || exit $?
   tail -2 gpurun_out/strip_pool_$P.log

@@ -77,6 +77,7 @@ for r in ranks:
             fh.export_flows(torch.from_numpy(halo.astype(np.int32)).to(dev), hf)
             hflows[torch.from_numpy(halo).to(dev)] = hf
             fh.pool_device()
+        ex_buf = torch.empty((1, 3), dtype=torch.float64, device=dev)
         cuts = np.searchsorted(sh.gidx, [b * n_stream // a.nsub for b in range(a.nsub + 1)])
         cuts[-1] = n
         subs = []
@@ -95,15 +96,24 @@ for r in ranks:
     def run():
         fm.reset()
         if sh.lists is not None:
+            # the order of multirank.Stepper.step: fit b+1, pool b, then the
+            # exchange of b+1 (its export waits for the fit; import)
             def fit(b):
-                lo, hi, hi_idx, hf = subs[b]
+                lo, hi, _, _ = subs[b]
                 fm.fit_device(dx[lo:hi], dy[lo:hi], dt[lo:hi], dp[lo:hi], {c: v[lo:hi] for c, v in out.items()})
+
+            def exchange(b):
+                _, _, hi_idx, hf = subs[b]
+                fm.export_flows(hi_idx[:1], ex_buf)
                 fm.import_flows(hi_idx, hf)
             fit(0)
+            exchange(0)
             for b in range(len(subs)):
                 if b + 1 < len(subs):
                     fit(b + 1)
                 fm.pool_device()
+                if b + 1 < len(subs):
+                    exchange(b + 1)
             return
         if a.split == "segments":
             fm.last_stamps(dx[o:], dy[o:], dt[o:], sh.n_head, mine[0], mine[1])

@@ -39,6 +39,13 @@ for S in $STAGES; do
     timeout -k 10 300 python3 -u tools/strip_rank.py --split segments --n 8 --ranks 3 \
       > gpurun_out/ranksim_segments_n8.log 2>&1
     rc=$?; echo "ranksim segments rc=$rc"; tail -1 gpurun_out/ranksim_segments_n8.log ;;
+  ab)  # device-resident C3 step for each "pool_chunk:pool_batch" in AB_CASES
+    for C in ${AB_CASES:-8192:64 4096:64 4096:128}; do
+      timeout -k 10 300 python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --host-steps 0 \
+        --pool-chunk ${C%%:*} --pool-batch ${C##*:} > gpurun_out/ab_${C/:/_}.log 2>&1
+      rc=$?; echo "ab $C rc=$rc"; grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_${C/:/_}.log
+      [ $rc -ne 0 ] && break
+    done ;;
   *) echo "unknown stage $S"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && exit $rc

@@ -199,7 +199,7 @@ struct Ctx {
     double *vx, *vy, *r_local, *th_local, *r_true, *th_true;
     int32_t *scale;
     int32_t *ox, *oy, *ot, *op;
-    unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells [3] cand [4] contrib
+    unsigned long long *counters;  // [0] n_valid [1] sae cells [2] pool cells [3] cand [4] contrib [5] owned
     int2 *dbg_tc;                  // profiling only: per event (candidates scanned, contributors)
 };
 
@@ -2194,7 +2194,7 @@ __global__ void k_last_time(const SaeCell *cells, int64_t WH, double *out) {
 // Algorithmic-work counters for the roofline: U_loc per event,
 // U_pool per valid event, valid count.  Grid-stride, one atomic per block.
 __global__ void k_stats(Ctx c) {
-    unsigned long long nv = 0, usae = 0, upool = 0, ncand = 0, ncon = 0;
+    unsigned long long nv = 0, usae = 0, upool = 0, ncand = 0, ncon = 0, nown = 0;
     const int fr = c.fr;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < c.n;
          e += (int64_t)gridDim.x * blockDim.x) {
@@ -2202,7 +2202,9 @@ __global__ void k_stats(Ctx c) {
         const int u0 = max(0, x - 2 * fr), u1 = min(c.W - 1, x + 2 * fr);
         const int v0 = max(0, y - 2 * fr), v1 = min(c.H - 1, y + 2 * fr);
         usae += (unsigned long long)(u1 - u0 + 1) * (unsigned long long)(v1 - v0 + 1);
-        if (c.valid[e] && x >= c.own_lo && x < c.own_hi) {
+        const bool own = x >= c.own_lo && x < c.own_hi;
+        nown += own;
+        if (c.valid[e] && own) {
             ++nv;
             if (c.dbg_tc) { const int2 tc = c.dbg_tc[e]; ncand += (unsigned)tc.x; ncon += (unsigned)tc.y; }
             const int i_lo = max(0, x - c.M), i_hi = min(c.W - 1, x + c.M);
@@ -2215,17 +2217,18 @@ __global__ void k_stats(Ctx c) {
             }
         }
     }
-    __shared__ unsigned long long s[5][256];
+    constexpr int NC = 6;
+    __shared__ unsigned long long s[NC][256];
     s[0][threadIdx.x] = nv; s[1][threadIdx.x] = usae; s[2][threadIdx.x] = upool;
-    s[3][threadIdx.x] = ncand; s[4][threadIdx.x] = ncon;
+    s[3][threadIdx.x] = ncand; s[4][threadIdx.x] = ncon; s[5][threadIdx.x] = nown;
     __syncthreads();
     for (int st = blockDim.x / 2; st > 0; st >>= 1) {
         if ((int)threadIdx.x < st)
-            for (int r = 0; r < 5; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
+            for (int r = 0; r < NC; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
         __syncthreads();
     }
     if (threadIdx.x == 0)
-        for (int r = 0; r < 5; ++r) atomicAdd(&c.counters[r], s[r][0]);
+        for (int r = 0; r < NC; ++r) atomicAdd(&c.counters[r], s[r][0]);
 }
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
@@ -2314,9 +2317,19 @@ struct farms_handle {
     bool profiling = false;  // kernel timing events
     bool counting = false;   // work counters (k_stats, per-event candidate counts)
     bool fit_events = false;  // timing events around every fit launch too
-    hipEvent_t ev[8] = {};
-    std::vector<hipEvent_t> kev;  // per-launch brackets of k_fit / k_pool when profiling
-    farms_stats stats{};
+    // Profiling across calls (farms_get_stats reports the calls since the last
+    // reset): each call records timing brackets -- its phases and its kernel
+    // launches -- on the streams that run them, synchronous or not; they are
+    // read (and their events recycled) when the stats are asked for, so that
+    // the asynchronous sub-batches of a pipelined step are counted too.
+    struct Bracket {
+        hipEvent_t a, b;
+        int kind;  // kBr* below
+    };
+    std::vector<Bracket> brk;
+    std::vector<hipEvent_t> ev_free;  // timing events ready for reuse
+    farms_stats acc{};                // totals of the brackets read so far, launch counts, counters
+    bool counters_dirty = false;      // k_stats ran since the counters were last read
     // host-array path (farms_process): pinned staging of inputs (16 B/event)
     // and records (52 B/event, or 68 with the x/y/t/p echo), an upload and a
     // download stream, one completion event per pooling super-chunk, one per
@@ -2402,6 +2415,77 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
     return FARMS_OK;
 }
 
+// Timing brackets (farms_handle::brk).
+enum { kBrPrep = 0, kBrFitSweep, kBrPoolSweep, kBrFitKernel, kBrPoolKernel };
+
+// Record a timing event (a recycled one when available) on stream s.
+int mark(farms_handle *h, hipStream_t s, hipEvent_t *out) {
+    if (!h->ev_free.empty()) {
+        *out = h->ev_free.back();
+        h->ev_free.pop_back();
+    } else {
+        HIPCHK(hipEventCreate(out));
+    }
+    HIPCHK(hipEventRecord(*out, s));
+    return FARMS_OK;
+}
+
+// Read every pending bracket into h->acc (waits for their end events), then
+// the work counters; the events go back to the free list.
+int harvest(farms_handle *h) {
+    std::vector<hipEvent_t> used;
+    used.reserve(2 * h->brk.size());
+    for (const auto &b : h->brk) {
+        HIPCHK(hipEventSynchronize(b.b));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, b.a, b.b));
+        switch (b.kind) {
+        case kBrPrep: h->acc.ms_prep += ms; break;
+        case kBrFitSweep: h->acc.ms_fit += ms; break;
+        case kBrPoolSweep: h->acc.ms_pool += ms; break;
+        case kBrFitKernel: h->acc.ms_fit_kernel += ms; break;
+        default: h->acc.ms_pool_kernel += ms; break;
+        }
+        used.push_back(b.a);
+        used.push_back(b.b);
+    }
+    h->brk.clear();
+    std::sort(used.begin(), used.end());
+    used.erase(std::unique(used.begin(), used.end()), used.end());
+    h->ev_free.insert(h->ev_free.end(), used.begin(), used.end());
+    h->acc.ms_total = h->acc.ms_prep + h->acc.ms_pool;
+    if (h->counters_dirty) {
+        for (hipStream_t s : {h->stream, h->s_chain, h->s_pool, h->s_copy})
+            if (s) HIPCHK(hipStreamSynchronize(s));
+        unsigned long long cnt[6];
+        HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemset(h->counters, 0, sizeof(cnt)));
+        h->acc.n_valid += (int64_t)cnt[0];
+        h->acc.sae_cells += (double)cnt[1];
+        h->acc.pool_cells += (double)cnt[2];
+        h->acc.pool_candidates += (double)cnt[3];
+        h->acc.pool_contributors += (double)cnt[4];
+        h->acc.n_owned += (int64_t)cnt[5];
+        h->counters_dirty = false;
+    }
+    return FARMS_OK;
+}
+
+// Forget the stats (farms_reset): drop the pending brackets, zero the counters.
+int clear_stats(farms_handle *h) {
+    for (const auto &b : h->brk) {
+        h->ev_free.push_back(b.a);
+        h->ev_free.push_back(b.b);
+    }
+    h->brk.clear();
+    std::sort(h->ev_free.begin(), h->ev_free.end());
+    h->ev_free.erase(std::unique(h->ev_free.begin(), h->ev_free.end()), h->ev_free.end());
+    h->acc = farms_stats{};
+    h->counters_dirty = false;
+    HIPCHK(hipMemset(h->counters, 0, sizeof(unsigned long long) * 8));
+    return FARMS_OK;
+}
+
 int reset_surfaces(farms_handle *h) {
     int rc = sync_all(h);
     if (rc) return rc;
@@ -2414,6 +2498,7 @@ int reset_surfaces(farms_handle *h) {
         HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
     }
     HIPCHK(hipStreamSynchronize(h->stream));
+    if ((rc = clear_stats(h))) return rc;
     h->seq = 0;
     h->chunk_base = h->super_base = 0;
     h->ph_count = 0;  // fits not pooled are dropped
@@ -2479,14 +2564,6 @@ bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t 
     return false;
 }
 
-int ensure_kernel_events(farms_handle *h, size_t count) {
-    while (h->kev.size() < count) {
-        hipEvent_t ev;
-        HIPCHK(hipEventCreate(&ev));
-        h->kev.push_back(ev);
-    }
-    return FARMS_OK;
-}
 
 int ensure_sync_events(Work &w, size_t count) {
     while (w.sync_ev.size() < count) {
@@ -2541,14 +2618,15 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.ox = dout->x; c.oy = dout->y; c.ot = dout->t; c.op = dout->p;
     if (!c.ox || !c.oy || !c.ot || !c.op) c.ox = c.oy = c.ot = c.op = nullptr;
     c.counters = h->counters;
-    c.dbg_tc = h->counting && !async ? w.dbg_tc : nullptr;
+    c.dbg_tc = h->counting ? w.dbg_tc : nullptr;
+    (void)async;
 
     return c;
 }
 
 // Before a call writes workspace set w: wait for the set's previous
 // asynchronous call, size its dependency events (and the profiling events).
-int claim_set(farms_handle *h, Work &w, int n, bool prof) {
+int claim_set(farms_handle *h, Work &w, int n, hipEvent_t *t_start) {
     hipStream_t s = h->stream;
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
     const int n_super = ceil_div(n_pool_chunks, h->pool_batch);
@@ -2556,18 +2634,18 @@ int claim_set(farms_handle *h, Work &w, int n, bool prof) {
         HIPCHK(hipStreamWaitEvent(s, w.done, 0));
         w.busy = false;
     }
-    if (prof) {
-        int rc = ensure_kernel_events(h, 2 * (size_t)(n_fit_chunks + n_super));
+    if (t_start) {  // profiled: the prep bracket opens here, after any wait
+        int rc = mark(h, s, t_start);
         if (rc) return rc;
-        HIPCHK(hipEventRecord(h->ev[0], s));
     }
     return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
 }
 
 // The prep of a call on set w (stream F): validate, pixel ids, sort by pixel,
 // links, fit descriptors, work order; records w.sync_ev[0].
-int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, bool prof) {
-    int rc = claim_set(h, w, n, prof);
+int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, hipEvent_t *t_prep) {
+    hipEvent_t t_start = nullptr;
+    int rc = claim_set(h, w, n, t_prep ? &t_start : nullptr);
     if (rc) return rc;
     hipStream_t s = h->stream;
     const int n_pool_chunks = ceil_div(n, h->pool_chunk);
@@ -2604,7 +2682,10 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     hipLaunchKernelGGL(k_fit_desc, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     HIPCHK(hipEventRecord(ev_prep, s));
-    if (prof) HIPCHK(hipEventRecord(h->ev[1], s));
+    if (t_prep) {
+        if ((rc = mark(h, s, t_prep))) return rc;
+        h->brk.push_back({t_start, *t_prep, kBrPrep});
+    }
     return FARMS_OK;
 }
 
@@ -2616,12 +2697,13 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     h->fresh = false;
     Ctx c = make_ctx(h, w, dx, dy, dt, dp, n, dout, async);
 
-    const bool prof = h->profiling && !async;
+    const bool prof = h->profiling;  // timing brackets, read by farms_get_stats (async calls too)
+    hipEvent_t t_prep = nullptr;     // prep done on F: the fit sweep's start
     const int n_fit_chunks = ceil_div(n, h->fit_chunk), n_pool_chunks = ceil_div(n, h->pool_chunk);
     const int B = h->pool_batch;
     const int n_super = ceil_div(n_pool_chunks, B);
     {
-        int rc = phase == 2 ? claim_set(h, w, n, prof) : enqueue_prep(h, w, c, n, validated, prof);
+        int rc = phase == 2 ? claim_set(h, w, n, nullptr) : enqueue_prep(h, w, c, n, validated, prof ? &t_prep : nullptr);
         if (rc) return rc;
     }
     // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
@@ -2630,10 +2712,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
     auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
     auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
-    if (phase == 2) {  // prepared by phase 1: its fits and the imported flows are in place at w.ready
-        if (prof) { HIPCHK(hipEventRecord(h->ev[1], s)); HIPCHK(hipEventRecord(h->ev[2], s)); }
-        ev_prep = w.ready;
-    }
+    if (phase == 2) ev_prep = w.ready;  // prepared by phase 1: its fits and the imported flows are in place
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
     //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
@@ -2678,7 +2757,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         cf.cells = cells_of(f);
         FitPrep next{};
         if (f + 1 < n_fit_chunks) next = prep_of(f + 1);
-        if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f], s));
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        if (prof && h->fit_events) { int rc = mark(h, s, &k0); if (rc) return rc; }
         bool merged = false;
         if (fast_fit) {
             merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
@@ -2687,7 +2767,11 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
                                c1 - c0);
         }
         if (!merged && next.blocks > 0) launch_prep(next);
-        if (prof && h->fit_events) HIPCHK(hipEventRecord(h->kev[2 * f + 1], s));
+        if (k0) {
+            int rc = mark(h, s, &k1);
+            if (rc) return rc;
+            h->brk.push_back({k0, k1, kBrFitKernel});
+        }
         HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
@@ -2698,11 +2782,18 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             fin.p0 = fit_start(std::max(f - 1, 0));
             fin.blocks = ceil_div(n - fin.p0, 64);
             launch_prep(fin);
-            if (prof) HIPCHK(hipEventRecord(h->ev[2], s));
+            if (t_prep && phase == 0) {  // the fit sweep's bracket (phase 1 closes it after k_flow)
+                hipEvent_t e2 = nullptr;
+                int rc = mark(h, s, &e2);
+                if (rc) return rc;
+                h->brk.push_back({t_prep, e2, kBrFitSweep});
+            }
         }
         return FARMS_OK;
     };
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
+    hipEvent_t t_pool0 = nullptr;  // the pooling sweep's start: the chain stream past the prep (phase 2: the fits)
+    if (prof && phase != 1) { int rc = mark(h, sc, &t_pool0); if (rc) return rc; }
     int fit_enqueued = 0, fit_waited = -1;
     if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
         while (fit_enqueued < n_fit_chunks) {
@@ -2710,13 +2801,17 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             if (rc) return rc;
         }
         hipLaunchKernelGGL(k_flow, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, 0, n);
+        if (t_prep) {
+            hipEvent_t e2 = nullptr;
+            int rc = mark(h, s, &e2);
+            if (rc) return rc;
+            h->brk.push_back({t_prep, e2, kBrFitSweep});
+        }
         HIPCHK(hipEventRecord(w.ready, s));
         if (!async) HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipGetLastError());
-        farms_stats st{};
-        st.n_events = n;
-        st.fit_launches = fit_launches;
-        h->stats = st;
+        h->acc.n_events += n;  // counted here; the pooling call (phase 2) counts its pooling work
+        h->acc.fit_launches += fit_launches;
         return FARMS_OK;
     }
     if (phase == 2) { fit_enqueued = n_fit_chunks; fit_waited = n_fit_chunks - 1; }  // fits done (phase 1)
@@ -2751,9 +2846,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         HIPCHK(hipEventRecord(ev_cand(S), sc));
         HIPCHK(hipStreamWaitEvent(sp, ev_cand(S), 0));
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S)], sp));
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        if (prof) { int rc = mark(h, sp, &k0); if (rc) return rc; }
         pl(c, p0, p1, sp);
-        if (prof) HIPCHK(hipEventRecord(h->kev[2 * ((size_t)n_fit_chunks + S) + 1], sp));
+        if (prof) {
+            int rc = mark(h, sp, &k1);
+            if (rc) return rc;
+            h->brk.push_back({k0, k1, kBrPoolKernel});
+        }
         // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
         hipLaunchKernelGGL(k_true_polar, dim3(ceil_div(p1 - p0, 256)), dim3(256), 0, sp, c, p0, p1);
         HIPCHK(hipEventRecord(ev_pool(S), sp));
@@ -2771,7 +2871,23 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     h->chunk_base += n_pool_chunks;
     if (n_super > 0) HIPCHK(hipEventRecord(h->chain_end, sc));
     HIPCHK(hipGetLastError());
-    const int pool_launches = n_super;
+    if (phase != 2) {
+        h->acc.n_events += n;
+        h->acc.fit_launches += fit_launches;
+    }
+    h->acc.pool_launches += n_super;
+    // the pooling sweep's bracket, and the work counters of the call's events
+    // (after its last pooling launch, before anything reuses the set)
+    if (t_pool0) {
+        hipEvent_t e3 = nullptr;
+        int rc = mark(h, sp, &e3);
+        if (rc) return rc;
+        h->brk.push_back({t_pool0, e3, kBrPoolSweep});
+    }
+    if (h->counting) {
+        hipLaunchKernelGGL(k_stats, dim3(1024), dim3(256), 0, sp, c);
+        h->counters_dirty = true;
+    }
     if (async && n_super > 0) {
         // w.done, on stream P after the last pooling launch (which follows the
         // chain's last step) and F's last work of the call (phase 2 has none):
@@ -2782,11 +2898,6 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         HIPCHK(hipEventRecord(w.done, sp));
         w.busy = true;
-        farms_stats st{};
-        st.n_events = n;
-        st.fit_launches = fit_launches;
-        st.pool_launches = pool_launches;
-        h->stats = st;
         return FARMS_OK;
     }
     // join: stream F waits for the last chain step and the last pooling launch
@@ -2794,61 +2905,20 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
     }
+    if (h->counting) {  // k_stats ran on P after the last pooling launch
+        hipEvent_t e4 = nullptr;
+        int rc = mark(h, sp, &e4);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(s, e4, 0));
+        h->ev_free.push_back(e4);
+    }
     if (async) {
         HIPCHK(hipEventRecord(w.done, s));
         w.busy = true;
-        farms_stats st{};
-        st.n_events = n;
-        st.fit_launches = fit_launches;
-        st.pool_launches = pool_launches;
-        h->stats = st;
         return FARMS_OK;
-    }
-    if (prof) HIPCHK(hipEventRecord(h->ev[3], s));
-    if (h->counting) {
-        HIPCHK(hipMemsetAsync(h->counters, 0, sizeof(unsigned long long) * 5, s));
-        hipLaunchKernelGGL(k_stats, dim3(1024), dim3(256), 0, s, c);
     }
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipGetLastError());
-
-    farms_stats st{};
-    st.n_events = n;
-    st.fit_launches = fit_launches;
-    st.pool_launches = pool_launches;
-    if (prof) {
-        float a = 0, b = 0, d = 0;
-        HIPCHK(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
-        HIPCHK(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
-        HIPCHK(hipEventElapsedTime(&d, h->ev[1], h->ev[3]));
-        // the fit and pooling sweeps overlap: ms_pool spans from the end of prep
-        // to the end of the last pooling launch
-        st.ms_prep = a; st.ms_fit = b; st.ms_pool = d; st.ms_total = (double)a + d;
-        double kf = 0, kp = 0;
-        for (int i = 0; i < (h->fit_events ? fit_launches : 0); ++i) {
-            float v = 0;
-            HIPCHK(hipEventElapsedTime(&v, h->kev[2 * i], h->kev[2 * i + 1]));
-            kf += v;
-        }
-        for (int i = 0; i < pool_launches; ++i) {
-            float v = 0;
-            const size_t ke = 2 * ((size_t)n_fit_chunks + i);  // one k_pool launch per super-chunk
-            HIPCHK(hipEventElapsedTime(&v, h->kev[ke], h->kev[ke + 1]));
-            kp += v;
-        }
-        st.ms_fit_kernel = kf;
-        st.ms_pool_kernel = kp;
-    }
-    if (h->counting) {
-        unsigned long long cnt[5];
-        HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
-        st.n_valid = (int64_t)cnt[0];
-        st.sae_cells = (double)cnt[1];
-        st.pool_cells = (double)cnt[2];
-        st.pool_candidates = (double)cnt[3];
-        st.pool_contributors = (double)cnt[4];
-    }
-    h->stats = st;
     return FARMS_OK;
 }
 
@@ -2964,8 +3034,6 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
-    for (auto &ev : h->ev)
-        if (hipEventCreate(&ev) != hipSuccess) return bail(fail(FARMS_EHIP, "hipEventCreate"));
     {
         std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end,
                                          };
@@ -3012,9 +3080,13 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->chain_end) (void)hipEventDestroy(h->chain_end);
     dfree(h->bw_ring);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
-    for (auto &ev : h->ev)
-        if (ev) (void)hipEventDestroy(ev);
-    for (auto &ev : h->kev) (void)hipEventDestroy(ev);
+    for (auto &b : h->brk) {
+        h->ev_free.push_back(b.a);
+        h->ev_free.push_back(b.b);
+    }
+    std::sort(h->ev_free.begin(), h->ev_free.end());
+    h->ev_free.erase(std::unique(h->ev_free.begin(), h->ev_free.end()), h->ev_free.end());
+    for (auto &ev : h->ev_free) (void)hipEventDestroy(ev);
     for (auto &ev : h->copy_ev) (void)hipEventDestroy(ev);
     for (auto &ev : h->final_ev) (void)hipEventDestroy(ev);
     if (h->s_copy) (void)hipStreamDestroy(h->s_copy);
@@ -3045,7 +3117,11 @@ extern "C" int farms_set_profiling(farms_handle *h, int enable) {
 
 extern "C" int farms_get_stats(const farms_handle *h, farms_stats *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
-    *out = h->stats;
+    farms_handle *m = const_cast<farms_handle *>(h);  // reads the pending brackets (opaque handle)
+    HIPCHK(hipSetDevice(h->prm.device));
+    int rc = harvest(m);
+    if (rc) return rc;
+    *out = h->acc;
     return FARMS_OK;
 }
 
@@ -3222,6 +3298,7 @@ extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const i
                                     const uint32_t *d_t, const int32_t *d_p, int64_t n, farms_records *d_out) {
     if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
     if (h->prm.import_halo) return fail(FARMS_EINVAL, "an import_halo handle runs farms_fit_device / farms_pool_device");
+    if (h->ph_count > 0) return fail(FARMS_EINVAL, "a farms_fit_device is waiting for farms_pool_device");
     if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
     if (n == 0) return FARMS_OK;
     if (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx || !d_out->vy ||
@@ -3319,6 +3396,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
                              const int32_t *p, int64_t n, farms_records *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");
     if (h->prm.import_halo) return fail(FARMS_EINVAL, "an import_halo handle runs farms_fit_device / farms_pool_device");
+    if (h->ph_count > 0) return fail(FARMS_EINVAL, "a farms_fit_device is waiting for farms_pool_device");
     if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
     if (n == 0) return FARMS_OK;
     if (!x || !y || !t || !p || !out->x || !out->y || !out->t || !out->p || !out->r_true || !out->theta_true ||
@@ -3395,6 +3473,13 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             hipEvent_t ev;
             HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             h->final_ev.push_back(ev);
+        }
+        // and one per sub-batch upload: every event exists before a thread is
+        // spawned, so an early return here never leaves a joinable thread
+        while ((int)h->up_ev.size() < nbat) {
+            hipEvent_t ev;
+            HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            h->up_ev.push_back(ev);
         }
     }
     struct Ready { int64_t S, p0, p1; };
@@ -3499,12 +3584,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     // asynchronous sub-batches unless the call is profiled (timing and counters
     // are read back per call)
     const bool async = !h->profiling && !h->counting;
-    int fit_launches = 0, pool_launches = 0;
-    while ((int)h->up_ev.size() < nbat) {
-        hipEvent_t ev;
-        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        h->up_ev.push_back(ev);
-    }
     // range check (vFlow.cpp:264 indexes the surfaces unchecked), staging and
     // upload of sub-batch b into the call's device copies (nothing to wait for)
     auto upload = [&](int b) -> int {
@@ -3568,8 +3647,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         rc = run_core(h, w, dev_in[0], dev_in[1], reinterpret_cast<const uint32_t *>(dev_in[2]), dev_in[3], m, &d,
                       &hook, 0, async, /*validated=*/true);
         if (rc) break;
-        fit_launches += h->stats.fit_launches;
-        pool_launches += h->stats.pool_launches;
         tr("enqueued", b);
     }
     if (trace) {  // when the device finished each stream's work
@@ -3583,9 +3660,6 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     tr("copy-out done", nbat);
     if (rc) return rc;
     if (bad) return fail(FARMS_EHIP, "farms_process: device-to-host copy");
-    h->stats.n_events = n;
-    h->stats.fit_launches = fit_launches;
-    h->stats.pool_launches = pool_launches;
     return FARMS_OK;
 }
 

@@ -9,6 +9,7 @@ or a GPU is missing, every call raises FarmsError.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 from dataclasses import dataclass
 
@@ -80,6 +81,7 @@ class FarmsStats(ctypes.Structure):
         ("ms_pool_kernel", ctypes.c_double),
         ("pool_candidates", ctypes.c_double),
         ("pool_contributors", ctypes.c_double),
+        ("n_owned", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -217,21 +219,20 @@ class Events:
 
 class PinnedArray:
     """A numpy array in pinned host memory (farms_host_alloc): farms_process
-    DMAs it in place instead of through its staging."""
+    DMAs it in place instead of through its staging.  The memory lives as long
+    as the ctypes buffer the array views (a finalizer on the buffer frees it),
+    so an array taken out of its PinnedArray, e.g. a column of
+    Records(pinned=True), keeps it alive by itself."""
 
     def __init__(self, n: int, dtype):
         lib = load_hip_library()
         self.dtype = np.dtype(dtype)
         p = ctypes.c_void_p()
         _check(lib, lib.farms_host_alloc(ctypes.c_int64(max(n, 1) * self.dtype.itemsize), ctypes.byref(p)))
-        self._p, self._lib = p, lib
         buf = (ctypes.c_char * (max(n, 1) * self.dtype.itemsize)).from_address(p.value)
+        # the ndarray holds buf through its base chain; free only when buf dies
+        weakref.finalize(buf, lib.farms_host_free, ctypes.c_void_p(p.value))
         self.array = np.frombuffer(buf, dtype=self.dtype, count=n)
-
-    def __del__(self):
-        if getattr(self, "_p", None) is not None and self._p.value:
-            self._lib.farms_host_free(self._p)
-            self._p = None
 
 
 def pinned(a: np.ndarray):

@@ -171,8 +171,12 @@ class Stepper:
             self.recv_x = self.recv_buf if same else {q: v.to(xdev) for q, v in self.recv_buf.items()}
             # sub-batches [lo, hi) of the stored events, cut at stream indices
             # G_b = b * n_stream / nsub; per sub-batch and peer the slices of
-            # the exchange lists and buffers, indices local to the sub-batch
-            nsub = max(1, min(nsub, sh.n)) if sh.n else 1
+            # the exchange lists and buffers, indices local to the sub-batch.
+            # nsub depends on nothing rank-local: every rank runs the same
+            # number of exchanges (a rank with fewer stored events than nsub
+            # gets empty sub-batches, which the engines accept), so the grouped
+            # send/recv pairs up on every rank.
+            nsub = max(1, int(nsub))
             cuts = np.searchsorted(sh.gidx, [b * sh.n_stream // nsub for b in range(nsub + 1)])
             cuts[-1] = sh.n
             self.sub = []

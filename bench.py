@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--host-steps", type=int, default=2,
                     help="N=1: steps of the host-array path (farms_process: H2D + kernels + D2H) timed after "
                          "the device-resident ones (0 = skip)")
+    ap.add_argument("--prof", choices=("timing", "pool"), default="timing",
+                    help="HIP-event brackets in the timed steps: around every fit and pooling launch (timing), or "
+                         "the pooling launches only (pool)")
     ap.add_argument("--plan-only", action="store_true",
                     help="launch, rendezvous, per-rank stream shares and partition only; no GPU, no timing "
                          "(CPU test of the multi-rank plumbing; value is null)")
@@ -139,51 +142,52 @@ def parity_vs_cpu(ref, out, k):
             "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"]}
 
 
-def committed_profile(kind: str, cfg: int, world: int, pool_launches: int, kernel: str):
-    """Per-kernel figures for the dominant kernel from the newest committed
-    rocprofv3 PMC summary of the same workload (profiles/rNN_<kind>_c<cfg>.json,
-    made by tools/gpu_traffic.sh / tools/gpu_sq.sh from `bench.py --steps 1
-    --warmup 0`).  None unless the profile saw whole steps of this launch count
-    (the same stream and chunking)."""
+def committed_profile(kind: str, cfg: int, split: str, kernel: str):
+    """Per-kernel PMC figures of the newest committed rocprofv3 summary of the
+    same per-GPU workload: profiles/rNN_<kind>_c<cfg>.json (tools/gpu_traffic.sh /
+    tools/gpu_sq.sh on `bench.py --config cfg --steps 1 --warmup 0`; a temporal
+    segment runs exactly that call) or, for x-strips,
+    profiles/rNN_<kind>_c<cfg>_strips.json (one rank-simulated strip step,
+    tools/strip_rank.py).  Per-launch figures: a launch covers a fixed number of
+    events (fit chunk / pooling super-chunk), whatever the stream length."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_c{cfg}.json")))
-    if world != 1 or not files:
+    suffix = "_strips" if split.startswith("strips") else ""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_c{cfg}{suffix}.json")))
+    if not files:
         return None
     k = json.load(open(files[-1]))["kernels"].get(kernel)
-    if not k or k["dispatches"] % pool_launches:
+    if not k:
         return None
     return dict(k, source=os.path.relpath(files[-1], ROOT))
 
 
-def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense_bytes: float) -> dict:
-    """Roofline of the dominant kernel, k_pool.
+def kernel_roofline(cfg: int, split: str, kernel: str, kname: str, launches: int, avg_us: float,
+                    algo_bytes_per_launch: float | None, binds: str) -> dict:
+    """Roofline of one hot kernel.
 
     achieved = HBM bytes per launch measured by the PMC counters (2 x
     FETCH_SIZE + WRITE_SIZE, the gfx950 correction) / the launch's average
-    duration, timed live with HIP events on the pooling stream; frac = achieved
-    / 8 TB/s.  The kernel is not HBM-bound (it reads a chunk's candidate lists
-    from L2): `binds` names what binds, latency, and `issue` gives its
-    measures from the SQ counters of the same workload (VALU issue
-    utilisation, wait fractions).  SURVEY §8d's dense-window figure (20 B per
-    window cell of a valid event) is reported apart as dense_equiv_*: the
-    kernel never reads the dense window, so that figure divided by the time
-    exceeds HBM peak and is no physical rate."""
-    jump, maxw = scales(cfg)
-    kname = f"k_pool<{maxw // jump + 1}>"
-    tr = committed_profile("traffic", cfg, world, pool_launches, kname)
-    sq = committed_profile("sq", cfg, world, pool_launches, kname)
+    duration, timed live with HIP events on the stream that runs it inside the
+    timed steps; frac = achieved / 8 TB/s.  Neither hot kernel is HBM-bound
+    (their working sets stay in L2): `binds` names what binds, and `issue`
+    gives the SQ counters of the same workload (VALU issue utilisation, wait
+    fractions).  `algorithmic_*` is SURVEY §8d's per-event figure over the
+    launch's events; for k_pool it counts the dense 101 x 101 window of every
+    valid event (20 B per cell), which the kernel never reads, so that
+    quotient is no physical rate and is never `frac`."""
+    tr = committed_profile("traffic", cfg, split, kname)
+    sq = committed_profile("sq", cfg, split, kname)
     traffic = round(tr["traffic_bytes_per_launch"]) if tr else None
     achieved = traffic / (avg_us * 1e-6) / 1e9 if traffic and avg_us > 0 else None
-    dense_per_launch = dense_bytes / max(pool_launches, 1)
     r = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
          "traffic_unit": "HBM bytes per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
          "traffic_source": tr["source"] if tr else None,
-         "kernel": "k_pool", "launches_per_step": pool_launches, "avg_launch_us": round(avg_us, 2),
-         "binds": "latency (dependent L2 loads and the fp64 fold chain), not HBM: see issue",
-         "dense_equiv_bytes_per_launch": round(dense_per_launch),
-         "dense_equiv_GBps": round(dense_per_launch / (avg_us * 1e-6) / 1e9, 1) if avg_us > 0 else None}
+         "kernel": kernel, "launches_per_step": launches, "avg_launch_us": round(avg_us, 2), "binds": binds}
+    if algo_bytes_per_launch is not None:
+        r["algorithmic_bytes_per_launch"] = round(algo_bytes_per_launch)
+        r["algorithmic_GBps"] = round(algo_bytes_per_launch / (avg_us * 1e-6) / 1e9, 1) if avg_us > 0 else None
     if sq and avg_us > 0:
         waves = max(sq["SQ_WAVES"], 1.0)
         wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
@@ -199,6 +203,33 @@ def pool_roofline(cfg: int, world: int, pool_launches: int, avg_us: float, dense
                       "source": sq["source"]}
         r["issue_frac"] = r["issue"]["valu_issue_util"]
     return r
+
+
+def rooflines(cfg: int, split: str, ts: dict, cs: dict) -> dict:
+    """Both hot kernels' rooflines from the timed steps' stats `ts` (HIP-event
+    launch brackets) and the counted step's `cs`, keyed "k_fit" / "k_pool";
+    "dominant" names the one with more kernel time per step (the pooling at
+    filtersize 5, the fit at filtersize 7)."""
+    fs = FILTER[cfg]
+    jump, maxw = scales(cfg)
+    nf, npl = max(ts["fit_launches"], 1), max(ts["pool_launches"], 1)
+    owned = max(cs["n_owned"], 1)
+    # SURVEY §8d per event: the fit reads 4 B per SAE cell of the clipped union
+    # (U_loc) and the 16-B event, and writes the plane (16 B) and its flag (1 B);
+    # pooling reads 20 B per dense window cell of a valid event (U_pool) and
+    # writes the 52-B record
+    fit_algo = (4.0 * cs["sae_cells"] + 33.0 * cs["n_events"]) / nf
+    pool_algo = (20.0 * cs["pool_cells"] + 52.0 * owned) / npl
+    out = {
+        "k_fit": kernel_roofline(cfg, split, "k_fit_quad", f"k_fit_quad<{fs // 2}>", ts["fit_launches"],
+                                 ts["ms_fit_kernel"] * 1e3 / nf, fit_algo,
+                                 "latency (dependent L2 loads of the SAE union window), not HBM: see issue"),
+        "k_pool": kernel_roofline(cfg, split, "k_pool", f"k_pool<{maxw // jump + 1}>", ts["pool_launches"],
+                                  ts["ms_pool_kernel"] * 1e3 / npl, pool_algo,
+                                  "latency (dependent L2 loads and the fp64 fold chain), not HBM: see issue"),
+    }
+    out["dominant"] = "k_fit" if ts["ms_fit_kernel"] > ts["ms_pool_kernel"] else "k_pool"
+    return out
 
 
 def host_path(fm, x, y, t, p, steps: int) -> dict:
@@ -352,8 +383,9 @@ def main():
     st = multirank.Stepper(fm, sh, dist, device, xdev)
     torch.cuda.synchronize()
 
-    # HIP events around the k_pool launches (and phases) only
-    fm.set_profiling(farms.PROF_POOL)
+    # HIP events around the phases and every fit and pooling launch, on the
+    # streams that run them (farms_stats sums them over a step's calls)
+    fm.set_profiling(farms.PROF_TIMING if args.prof == "timing" else farms.PROF_POOL)
     if dist:
         dist.barrier()  # communicators up on every rank before the first exchange
     for _ in range(args.warmup):
@@ -367,6 +399,7 @@ def main():
         st.step()
         stats.append(fm.stats())
     torch.cuda.synchronize()
+    elapsed_rank = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -382,16 +415,34 @@ def main():
 
     ms_step = elapsed / args.steps * 1e3
     value = total_events * args.steps / elapsed / 1e6
-    pool_ms = sum(s["ms_pool_kernel"] for s in stats) / len(stats)
-    ts = stats[-1]  # timings of the last timed step
-    pool_launches = ts["pool_launches"]
-    # work counters (U_pool, candidates, contributors) from one more, untimed step
+    mean = {k: sum(s_[k] for s_ in stats) / len(stats) for k in ("ms_fit_kernel", "ms_pool_kernel")}
+    ts = dict(stats[-1], **mean)  # launch counts of a step, kernel times averaged over the timed steps
+    # work counters (U_loc, U_pool, candidates, contributors) from one more, untimed step
     fm.set_profiling(True)
     st.step()
     cs = fm.stats()
-    avg_us = pool_ms * 1e3 / max(pool_launches, 1)
-    dense_bytes = 20.0 * cs["pool_cells"]  # 20 B per dense pooling-window cell of a valid event
-    roofline = pool_roofline(cfg, world, pool_launches, avg_us, dense_bytes)
+    rl = rooflines(cfg, args.split, ts, cs)
+    dom = rl["dominant"]
+    mine = {"rank": rank, "ms_step_rank": round(elapsed_rank / args.steps * 1e3, 3),
+            "stored_events": n, "owned_events": n_owned,
+            "valid_frac": round(cs["n_valid"] / max(cs["n_owned"], 1), 4),
+            "dominant": dom, "avg_launch_us": {k: rl[k]["avg_launch_us"] for k in ("k_fit", "k_pool")},
+            "frac": {k: rl[k]["frac"] for k in ("k_fit", "k_pool")},
+            "ms_fit_kernel": round(ts["ms_fit_kernel"], 3), "ms_pool_kernel": round(ts["ms_pool_kernel"], 3)}
+    per_rank = [mine]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    # the line's roofline: rank 0's dominant kernel, with every rank's figures
+    # (per_rank) and the slowest rank named
+    roofline = dict(rl[dom])
+    if world > 1:
+        roofline["rank"] = rank
+        roofline["critical_rank"] = max(per_rank, key=lambda r: r["ms_step_rank"])["rank"]
+        roofline["per_rank"] = per_rank
+    roofline["other"] = {k: {f: rl[k].get(f) for f in ("kernel", "frac", "achieved", "avg_launch_us",
+                                                        "launches_per_step", "traffic_source")}
+                         for k in ("k_fit", "k_pool") if k != dom}
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
@@ -401,11 +452,13 @@ def main():
                    "events_per_gpu": per_gpu, "width": W, "height": H, "filtersize": fs,
                    "parallelism": sh.label},
         "roofline": roofline,
-        "detail": {"valid_frac": round(cs["n_valid"] / max(cs["n_events"], 1), 4),
+        "detail": {"valid_frac": round(cs["n_valid"] / max(cs["n_owned"], 1), 4),
                    "ms_prep": round(ts["ms_prep"], 3), "ms_fit_sweep": round(ts["ms_fit"], 3),
-                   "ms_pool_sweep": round(ts["ms_pool"], 3), "ms_pool_kernel": round(pool_ms, 3),
-                   "ms_fit_kernel_untimed_step": round(cs["ms_fit_kernel"], 3),
-                   "dense_equiv_bytes_per_event": round(dense_bytes / max(n, 1), 1),
+                   "ms_pool_sweep": round(ts["ms_pool"], 3), "ms_fit_kernel": round(ts["ms_fit_kernel"], 3),
+                   "ms_pool_kernel": round(ts["ms_pool_kernel"], 3),
+                   "fit_launches": ts["fit_launches"], "pool_launches": ts["pool_launches"],
+                   "profiling": args.prof,
+                   "dense_equiv_bytes_per_event": round(20.0 * cs["pool_cells"] / max(n_owned, 1), 1),
                    "cand_per_valid": round(cs["pool_candidates"] / max(cs["n_valid"], 1), 1),
                    "contrib_per_valid": round(cs["pool_contributors"] / max(cs["n_valid"], 1), 1)},
     }

@@ -85,7 +85,9 @@ typedef struct {
     int32_t *scale;
 } farms_records;
 
-/* Counters of the most recent farms_process* call. */
+/* Counters of every farms_process* / farms_fit_device / farms_pool_device call
+ * since the last farms_reset (or farms_create): asynchronous and pipelined calls
+ * included.  farms_get_stats waits for the profiled work it reports. */
 typedef struct {
     int64_t n_events;
     int64_t n_valid;         /* events that passed the validity gate (vFlow.cpp:315) */
@@ -99,6 +101,7 @@ typedef struct {
     double ms_pool_kernel;  /* sum of k_pool launch durations */
     double pool_candidates;   /* sum over valid events of candidate cells scanned */
     double pool_contributors; /* sum over valid events of contributing cells (largest scale) */
+    int64_t n_owned;          /* events in the owned columns (all of them unless own_x1 is set) */
 } farms_stats;
 
 /* vFlowManager ctor defaults: 320 x 320, filter 3, 5 inliers (main.cpp:21-24),
@@ -154,8 +157,9 @@ int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, con
 int farms_pool_device(farms_handle *h);
 
 /* Profiling of the next calls: FARMS_PROF_TIMING records HIP events around the
- * phases and every k_fit / k_pool launch (times in farms_stats; ~1,700 event
- * records per 50M events, a few % of a call), FARMS_PROF_POOL only around the
+ * phases and every k_fit / k_pool launch on the stream that runs it (times in
+ * farms_stats, summed over the calls since the last reset; ~1,700 event records
+ * per 50M events), FARMS_PROF_POOL only around the
  * phases and the k_pool launches (ms_fit_kernel stays 0), FARMS_PROF_COUNTERS
  * also counts U_loc / U_pool / candidates / contributors (an extra kernel
  * pass, ~2% of a call).  0 = off (default); any other value = timing and

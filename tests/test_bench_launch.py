@@ -75,3 +75,28 @@ def test_strip_plan_from_histogram_equals_plan_from_events():
     a = strips.plan(ev.x, 320, 320, 4, 5, 50)
     b = strips.plan_hist(np.bincount(ev.x, minlength=320), 320, 4, 5, 50)
     assert a == b
+
+
+def test_rooflines_name_the_dominant_kernel_per_config():
+    """bench.py reports the roofline of the kernel with more time per step (the
+    pooling at filtersize 5, the fit at filtersize 7), with the other kernel's
+    figures beside it, from live launch timings and the committed PMC summary
+    of the same per-GPU workload (none committed for a config: frac null)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ts = {"fit_launches": 100, "pool_launches": 10, "ms_fit_kernel": 50.0, "ms_pool_kernel": 20.0}
+    cs = {"n_events": 1000, "n_owned": 1000, "n_valid": 400, "sae_cells": 169e3, "pool_cells": 4e6}
+    rl = bench.rooflines(4, "segments", ts, cs)
+    assert rl["dominant"] == "k_fit"
+    assert rl["k_fit"]["avg_launch_us"] == 500.0 and rl["k_pool"]["avg_launch_us"] == 2000.0
+    assert rl["k_fit"]["algorithmic_bytes_per_launch"] == round((4 * 169e3 + 33 * 1000) / 100)
+    ts.update(ms_fit_kernel=10.0)
+    rl = bench.rooflines(3, "segments", ts, cs)
+    assert rl["dominant"] == "k_pool"
+    for k in ("k_fit", "k_pool"):
+        r = rl[k]
+        if r["traffic"]:
+            assert r["frac"] == round(r["traffic"] / (r["avg_launch_us"] * 1e-6) / 1e9 / 8000.0, 4)
+        else:
+            assert r["frac"] is None

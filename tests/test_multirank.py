@@ -124,7 +124,10 @@ def _rank_main(rank, world, port, cfg, per_rank, split, q, engine="oracle"):
 
 
 @pytest.mark.parametrize("split,world,cfg,per_rank", [("segments", 3, 2, 20_000), ("strips", 3, 2, 20_000),
-                                                      ("strips", 2, 3, 25_000), ("strips-recompute", 2, 3, 25_000)])
+                                                      ("strips", 2, 3, 25_000), ("strips-recompute", 2, 3, 25_000),
+                                                      # strips storing fewer events than the 8 sub-batches of a step:
+                                                      # every rank still runs 8 exchanges (empty sub-batches)
+                                                      ("strips", 3, 2, 3)])
 def test_gloo_ranks_with_the_oracle_engine_reproduce_the_whole_run(split, world, cfg, per_rank):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -148,6 +151,8 @@ def test_gloo_ranks_with_the_oracle_engine_reproduce_the_whole_run(split, world,
     rep = multi_report(merged, whole, whole, bnd)
     print(label, rep)
     assert rep["ok"], rep
+    if per_rank < 100:  # the tiny stream: too few events for valid flows at every border
+        return
     for b in rep["boundaries"]:
         assert b["events"] > 0 and b["valid_events"] > 0 and b["bitwise_vs_cr_oracle"]
 

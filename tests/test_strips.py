@@ -236,6 +236,37 @@ def test_import_halo_handle_guards():
 
 
 @pytest.mark.gpu
+def test_one_phase_calls_refused_while_a_fit_waits_for_its_pooling():
+    """A one-phase call between farms_fit_device and farms_pool_device would
+    reuse the pending fit's workspace set (its flows and validity): refused,
+    and the pending fit still pools to the same records as one call."""
+    W, H, fs = 320, 320, 5
+    ev = farms.synth_config(2, 60_000)
+    x, y, t, p = ev.relative()
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x, y, t.view(np.int32), p)]
+
+    def outs():
+        return {c: torch.zeros(len(x), dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+                for c in COLS[4:]}
+    with farms.FlowManager(H, W, fs, 5) as fm:
+        whole = outs()
+        fm.process_device(*d, whole)
+        fm.reset()
+        o = outs()
+        fm.fit_device(*d, o)
+        for call in (lambda: fm.process_device(*d, outs()), lambda: fm.process(x, y, t, p)):
+            with pytest.raises(farms.FarmsError) as ei:
+                call()
+            assert ei.value.code == farms.FARMS_EINVAL
+        fm.pool_device()
+    for c in COLS[4:]:
+        a, b = whole[c].cpu().numpy(), o[c].cpu().numpy()
+        assert np.array_equal(a.view(np.int64) if a.dtype == np.float64 else a,
+                              b.view(np.int64) if b.dtype == np.float64 else b), c
+
+
+@pytest.mark.gpu
 def test_engine_strips_narrow_and_short_sensors():
     """Strips narrower than the halo (flows from two ranks away) on a square
     sensor, and a sensor lower than maxWindow where the W-1 clip reaches two

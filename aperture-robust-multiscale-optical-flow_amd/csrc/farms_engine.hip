@@ -90,22 +90,34 @@ struct __attribute__((aligned(32))) FlowCell {
     uint32_t pad;
 };
 
-// SAE cell (x-major, 32 B, two 16-B loads): snapshot of the SAE at chunk start
-// plus the first two events of the current chunk at this pixel, inline, so
-// "stamp as of e" is resolved without pointer chasing unless the pixel fired
-// three or more times in the chunk (a bar's ON/OFF pair is the common case).
-// tag: bit31 = snapshot visited, bits 0..30 = seq of the chunk that last touched
-// the pixel.  e1m: first in-chunk event id, bit31 = more than one in-chunk event.
-// e2m: second in-chunk event id, bit31 = more than two (then the pixel's run
-// [run_lo, run_hi] of positions in P, scanned in PT, resolves later events).
-struct __attribute__((aligned(16))) SaeCell {
+// SAE cell (x-major): snapshot of the SAE at chunk start plus the first two
+// events of the current chunk at this pixel, inline, so "stamp as of e" is
+// resolved without pointer chasing unless the pixel fired three or more times
+// in the chunk (a bar's ON/OFF pair is the common case).  Two arrays of 16-B
+// records: the head, read by every window scan (eight cells per 128-B line,
+// so the four lanes of a fit quad reading four consecutive rows touch one
+// line), and the tail, read only when a pixel fired twice in the chunk.
+// head: tag: bit31 = snapshot visited, bits 0..30 = seq of the chunk that last
+//   touched the pixel; e1m: first in-chunk event id, bit31 = more than one
+//   in-chunk event; t1: its stamp; tsnap: the snapshot stamp.
+// tail: e2m: second in-chunk event id, bit31 = more than two (then the pixel's
+//   run [run_lo, run_hi] of positions in P, scanned in PT, resolves later
+//   events); t2: its stamp.
+struct __attribute__((aligned(16))) SaeHead {
     uint32_t tag;
     uint32_t e1m;
     uint32_t t1;
     uint32_t tsnap;
+};
+struct __attribute__((aligned(16))) SaeTail {
     uint32_t e2m;
     uint32_t t2;
     int32_t run_lo, run_hi;
+};
+// One SAE buffer: WH heads and WH tails.
+struct SaeBuf {
+    SaeHead *head;
+    SaeTail *tail;
 };
 
 // Pooling candidate: one cell of the per-chunk bitmap, its flow state before
@@ -172,7 +184,7 @@ struct Ctx {
     // the pixel's first event of the call, the snapshot's in serial mode, 0 in
     // batch mode, where it is not read)
     const int4 *link;
-    SaeCell *cells;        // SAE snapshot + in-chunk first event, per cell
+    SaeBuf cells;          // SAE snapshot + in-chunk first events, per cell (the fit chunk's buffer)
     const int2 *PT;        // per position in P: {event id, t}
     FlowCell *fsnap;       // flow snapshot
     int64_t *ftime;        // fsnap.L > 0 ? fsnap.t : -1  (bitmap pre-filter)
@@ -225,7 +237,7 @@ __device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint4 h, uint32_t
         const int e1 = (int)(h.y & kSeqMask);
         if (e1 <= e) {
             if (!(h.y >> 31)) return (int64_t)h.z;
-            const uint4 g = reinterpret_cast<const uint4 *>(c.cells)[2 * (size_t)q + 1];  // e2m, t2, run_lo, run_hi
+            const uint4 g = reinterpret_cast<const uint4 *>(c.cells.tail)[q];  // e2m, t2, run_lo, run_hi
             if ((int)(g.x & kSeqMask) > e) return (int64_t)h.z;
             if (!(g.x >> 31)) return (int64_t)g.y;
             return (int64_t)run_asof(c, (int)g.z, (int)g.w, e, g.y);
@@ -235,7 +247,7 @@ __device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint4 h, uint32_t
 }
 
 __device__ __forceinline__ uint4 sae_head(const Ctx &c, uint32_t q) {
-    return reinterpret_cast<const uint4 *>(c.cells)[2 * (size_t)q];
+    return reinterpret_cast<const uint4 *>(c.cells.head)[q];
 }
 
 __device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
@@ -358,15 +370,15 @@ __global__ void k_chunk_minmax(const uint32_t *t, int n, int chunk, uint32_t *tm
 // it (chunks f-2 and f-1: the buffer last served chunk f-2), set the snapshot
 // of the pixels they touched that chunk f does not touch to their last event.
 // The two parts write disjoint cells.
-__device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq,
+__device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeBuf cells, int p0, int c0, int c1, uint32_t seq,
                                                 int i) {
     const int ep = p0 + i;
     if (ep < c0) {
         const int nx = c.link[ep].z;
         if (nx >= c0 && nx >= c1) {  // last event of chunk f-1 at a pixel chunk f does not touch
-            SaeCell *cell = &cells[c.pix[ep]];
-            cell->tag |= 0x80000000u;
-            cell->tsnap = c.t[ep];
+            SaeHead *hd = &cells.head[c.pix[ep]];
+            hd->tag |= 0x80000000u;
+            hd->tsnap = c.t[ep];
         }
     }
     const int e = c0 + i;
@@ -375,23 +387,24 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeCell *cells, in
     const int4 lk = c.link[e];  // {pos, prev, next, stamp before}
     const int nx = lk.z;
     if (lk.y < c0) {  // first event of the pixel in the chunk
-        SaeCell *cell = &cells[q];
+        SaeHead *hd = &cells.head[q];
+        SaeTail *tl = &cells.tail[q];
         if (lk.y >= 0) {
-            cell->tag = seq | 0x80000000u;
-            cell->tsnap = (uint32_t)lk.w;
+            hd->tag = seq | 0x80000000u;
+            hd->tsnap = (uint32_t)lk.w;
         } else {  // no earlier event in this call: keep the snapshot of earlier calls
-            cell->tag = (cell->tag & 0x80000000u) | seq;
+            hd->tag = (hd->tag & 0x80000000u) | seq;
         }
-        cell->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
-        cell->t1 = c.t[e];
-        cell->run_lo = lk.x;
+        hd->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
+        hd->t1 = c.t[e];
+        tl->run_lo = lk.x;
         if (nx < c1) {  // and the second one
             const int nn = c.link[nx].z;
-            cell->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
-            cell->t2 = c.t[nx];
+            tl->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
+            tl->t2 = c.t[nx];
         }
     }
-    if (nx >= c1) cells[q].run_hi = lk.x;
+    if (nx >= c1) cells.tail[q].run_hi = lk.x;
 }
 
 // Pooling descriptors of work-order positions [p0, p1): {event, x, y, t}, the
@@ -419,7 +432,7 @@ __global__ void k_fit_desc(Ctx c) {
 
 // The prep of one fit chunk as its own launch (the first chunk of a call, the
 // final commits, the fit paths without a merged prep).
-__global__ void k_fit_prep(Ctx c, SaeCell *cells, int p0, int c0, int c1, uint32_t seq) {
+__global__ void k_fit_prep(Ctx c, SaeBuf cells, int p0, int c0, int c1, uint32_t seq) {
     fit_prep_thread(c, cells, p0, c0, c1, seq, (int)(blockIdx.x * blockDim.x + threadIdx.x));
 }
 
@@ -429,7 +442,7 @@ __global__ void k_fit_prep(Ctx c, SaeCell *cells, int p0, int c0, int c1, uint32
 // of chunk f does not read, and the fit of chunk f-1 (the buffer's last reader)
 // finished with the previous launch.
 struct FitPrep {
-    SaeCell *cells;
+    SaeBuf cells;
     int p0, c0, c1;
     uint32_t seq;
     int blocks;  // prep blocks after the fit's
@@ -1268,8 +1281,200 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     acc_out = true;
 }
 
+// Variant with rows per lane: lane j of the quad scans union rows j, j + 4, ...
+// over every union column, so in each load instruction the quad's four lanes
+// read four consecutive rows of one column -- consecutive x-major cells, one
+// 64-B span of the SAE head array -- where the column mapping reads four cells
+// a column (H cells) apart.  Scores, union tile and results as in
+// fit_event_quad_u; the visited bits are kept row-major (bit (row slot) * US +
+// column of the union, then cyo * side + cxo of the window).
+template <int FR>
+__device__ __forceinline__ void fit_event_quad_r(const Ctx &c, int4 fd, uint32_t seq, int j, uint32_t *ut, double &vx_out,
+                                                 double &vy_out, bool &acc_out) {
+    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
+    constexpr int NR = (US + 3) / 4;  // union rows per lane (the last one absent on some lanes)
+    static_assert(NR * US <= 64, "visited bits of a lane's union cells in one word");
+    const int W = c.W, H = c.H;
+    const int e = fd.x, ex = fd.y, ey = fd.z;  // the fit descriptor (k_fit_desc)
+    const uint32_t te = (uint32_t)fd.w;
+    vx_out = 0.0;
+    vy_out = 0.0;
+    acc_out = false;
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
+        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    if (!any) return;  // uniform over the quad
+    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union rows
+    uint64_t umask = 0;  // visited bits: (row slot) * US + union column
+    const int v0 = ey - 2 * FR;
+#pragma unroll 1
+    for (int cb = 0; cb < US; cb += 3) {  // three union columns at a time: their loads in flight together
+        uint4 col[3][NR];
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+            const int ucol = cb + cc;
+            const int u = ex + ucol - 2 * FR;
+            const bool inr = ucol < US && u >= 0 && u < W && u >= c.X0 && u < c.XR1;  // outside the stored region: never visited
+            const int cbase = (u - c.X0) * H + v0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int i = j + 4 * r, v = v0 + i;
+                // unconditional load from a clamped index, then select (a load
+                // under a branch is waited for at the branch end)
+                const bool ok = inr && i < US && v >= 0 && v < H;
+                const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+                col[cc][r] = ok ? hd : make_uint4(0, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+            const int ucol = cb + cc;
+            const int u = ex + ucol - 2 * FR;
+            if (ucol >= US || u < 0 || u >= W) continue;
+            int64_t sv[3] = {0, 0, 0};  // this lane's part of the column sum of each window row range
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int i = j + 4 * r, v = v0 + i;
+                if (i >= US || v < 0 || v >= H) continue;
+                const int64_t st = sae_resolve_h(c, col[cc][r], (uint32_t)((u - c.X0) * H + v), e, seq);
+                const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+                ut[(ucol * US + i) * kFitQS] = tk;
+                umask |= st >= 0 ? 1ull << (r * US + ucol) : 0ull;
+                const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+                for (int ovi = 0; ovi < 3; ++ovi)
+                    if (i >= ovi * FR && i <= ovi * FR + 2 * FR) sv[ovi] += d;
+            }
+            const int du = ucol - 2 * FR;
+#pragma unroll
+            for (int oui = 0; oui < 3; ++oui) {
+                const int ou = (oui - 1) * FR;
+                if (du - ou <= FR && ou - du <= FR) {
+#pragma unroll
+                    for (int ovi = 0; ovi < 3; ++ovi) score[oui * 3 + ovi] += sv[ovi];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) score[w] = quad_sum_i64(score[w]);
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
+
+    // ---- the winning window (vFlow.cpp:923-930) from the union tile: visited
+    // bits of the window rows this lane holds (row-major, bit cyo * side +
+    // cxo), combined over the quad
+    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
+    const int ub = (bw / 3) * FR, vb = (bw % 3) * FR;  // window origin in the union
+    uint64_t vis = 0;
+#pragma unroll
+    for (int cyo = 0; cyo < side; ++cyo) {
+        const int ur = vb + cyo;
+        if ((ur & 3) != j) continue;
+        const uint64_t rowbits = (umask >> ((ur >> 2) * US + ub)) & ((1ull << side) - 1);
+        vis |= rowbits << (cyo * side);
+    }
+    vis = quad_or_u64(vis);
+    // the union stamps were written by the other lanes of this wave's quad
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {  // k in the reference order: cx-major
+        const int kx = k / side, ky = k % side;
+        const int cx = bi + kx - FR, cy = bj + ky - FR;
+        const bool vk = (vis >> (ky * side + kx)) & 1;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = ut[((ub + kx) * US + vb + ky) * kFitQS];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
+    syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    if (DET < 1) return;  // 0 inliers; uniform over the quad
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);  // (d2, d5, d8: the intercept row, never used)
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    // (A2 * At) * Y in the reference order (r2, the intercept, is never used:
+    // vFlow.cpp:1352-1377).  Each term m_k * yt_k is one rounded product,
+    // independent of the others, so lane j of the quad forms the terms of
+    // cells k = kb + j, and the sums then add them in order k = 0, 1, ... on
+    // every lane (quad broadcasts): the additions are the reference's, a quarter
+    // of the products per lane.
+    double r0 = 0.0, r1 = 0.0;
+#pragma unroll 1
+    for (int kb = 0; kb < np; kb += 4) {
+        const int k = kb + j < np ? kb + j : np - 1;
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+        }
+        const double q0 = m0 * yt, q1 = m1 * yt;
+        const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
+        if (!gemv && kb == 0) { r0 = a0; r1 = a1; }
+        else { r0 = r0 + a0; r1 = r1 + a1; }
+        if (kb + 1 < np) { r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1); }
+        if (kb + 2 < np) { r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1); }
+        if (kb + 3 < np) { r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1); }
+    }
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    inliers += xch32<0>(inliers);
+    inliers += xch32<1>(inliers);
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
+}
+
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
-template <int FR, bool UT>
+// (MODE 0: re-gather the winning window; 1: union tile, columns per lane;
+// 2: union tile, rows per lane)
+template <int FR, int MODE>
 __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
     const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
     if ((int)blockIdx.x >= G) {
@@ -1278,7 +1483,7 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
         return;
     }
     const int bid = (int)blockIdx.x;
-    constexpr int NPC = UT ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
+    constexpr int NPC = MODE ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
     // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
@@ -1291,8 +1496,259 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
     if (!c.fit_all && (fd.y < c.fit_lo || fd.y >= c.fit_hi)) return;
     double vx, vy;
     bool acc;
-    if constexpr (UT) fit_event_quad_u<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    if constexpr (MODE == 2) fit_event_quad_r<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    else if constexpr (MODE == 1) fit_event_quad_u<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
     else fit_event_quad<FR>(c, fd, seq, j, s_tk + (threadIdx.x >> 2), vx, vy, acc);
+    if (j == 0) fit_plane(c, fd.x, vx, vy, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Box variant (MODE 3): the 16 events of a fit wave are neighbours in tile
+// order, so their union windows overlap.  The wave loads the SAE heads of the
+// bounding box of its events' union windows into LDS once (consecutive lanes
+// read consecutive rows of a column: consecutive x-major cells), and every
+// quad resolves its cells from there instead of issuing its own global loads
+// (81 / 169 per event at filter 5 / 7).  Events past the box's capacity (the
+// greedy prefix of the wave's quads whose bounding box fits) read the global
+// heads as before.  The box holds heads only: "as of e" is resolved per event
+// (sae_resolve_h, whose rare second-event lookups read the tail array).
+// Scores are exact int64 sums in any order; the winning window is resolved
+// again by each lane for its own cells k = j, j + 4, ... (registers), which is
+// what the AtA sums, the ordered (A2 * At) * Y terms and the inlier test read
+// (a window tile of np x 16 stamps past the box; no union tile).
+template <int FR> struct FitBox {
+    static constexpr int CAP = FR == 1 ? 320 : FR == 2 ? 576 : 768;  // 16-B LDS slots per wave
+    static constexpr int WT = ((2 * FR + 1) * (2 * FR + 1) * kFitQS + 3) / 4;  // of them for the window tile
+    static constexpr int BOX = CAP - WT;  // box cells
+};
+
+template <int FR>
+__device__ __forceinline__ void fit_event_box(const Ctx &c, int4 fd, uint32_t seq, int j, bool inbox, int BX0, int BY0,
+                                              int BH, const uint4 *box, uint32_t *wt, double &vx_out, double &vy_out,
+                                              bool &acc_out) {
+    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
+    constexpr int NR = (US + 3) / 4;   // union rows per lane
+    const int W = c.W, H = c.H;
+    const int e = fd.x, ex = fd.y, ey = fd.z;
+    const uint32_t te = (uint32_t)fd.w;
+    vx_out = 0.0;
+    vy_out = 0.0;
+    acc_out = false;
+    bool wok[9];
+    int64_t score[9];
+    bool any = false;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
+        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
+        score[w] = 0;
+        any |= wok[w];
+    }
+    if (!any) return;  // uniform over the quad
+    // head of cell (u, v), zero outside the sensor / the stored region: from
+    // the box, or (events past its capacity) from global memory, an
+    // unconditional load from a clamped index
+    auto head_at = [&](int u, int v) -> uint4 {
+        const bool ok = u >= 0 && u < W && u >= c.X0 && u < c.XR1 && v >= 0 && v < H;
+        uint4 hd;
+        if (inbox) hd = box[(u - BX0) * BH + (v - BY0)];
+        else hd = sae_head(c, ok ? (uint32_t)((u - c.X0) * H + v) : 0u);
+        return ok ? hd : make_uint4(0, 0, 0, 0);
+    };
+    // ---- window scores (vFlow.cpp:870-912): this lane's union rows j, j + 4, ...
+    const int v0 = ey - 2 * FR;
+#pragma unroll 1
+    for (int ucol = 0; ucol < US; ++ucol) {
+        const int u = ex + ucol - 2 * FR;
+        uint4 hc[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int i = j + 4 * r;
+            hc[r] = head_at(u, i < US ? v0 + i : -1);
+        }
+        if (u < 0 || u >= W) continue;
+        int64_t sv[3] = {0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int i = j + 4 * r, v = v0 + i;
+            if (i >= US || v < 0 || v >= H) continue;
+            const int64_t st = sae_resolve_h(c, hc[r], (uint32_t)((u - c.X0) * H + v), e, seq);
+            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+#pragma unroll
+            for (int ovi = 0; ovi < 3; ++ovi)
+                if (i >= ovi * FR && i <= ovi * FR + 2 * FR) sv[ovi] += d;
+        }
+        const int du = ucol - 2 * FR;
+#pragma unroll
+        for (int oui = 0; oui < 3; ++oui) {
+            const int ou = (oui - 1) * FR;
+            if (du - ou <= FR && ou - du <= FR) {
+#pragma unroll
+                for (int ovi = 0; ovi < 3; ++ovi) score[oui * 3 + ovi] += sv[ovi];
+            }
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < 9; ++w) score[w] = quad_sum_i64(score[w]);
+    const int64_t nn = np;
+    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
+    int bw = -1;
+#pragma unroll
+    for (int w = 0; w < 9; ++w)
+        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
+    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
+
+    // ---- the winning window, cx-major (vFlow.cpp:923-930): this lane resolves
+    // its cells k = j, j + 4, ... into the quad's window tile wt (stride 16,
+    // past the box) and their visited bits, combined over the quad
+    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
+    uint64_t vis = 0;
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        const int u = bi + k / side - FR, v = bj + k % side - FR;
+        const int64_t st = sae_resolve_h(c, head_at(u, v), (uint32_t)((u - c.X0) * H + v), e, seq);
+        wt[k * kFitQS] = st < 0 ? 0u : (uint32_t)st;
+        vis |= st >= 0 ? 1ull << k : 0ull;
+    }
+    vis = quad_or_u64(vis);
+    // the window's stamps were written by the other lanes of this wave's quad
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {  // k in the reference order: cx-major
+        const int cx = bi + k / side - FR, cy = bj + k % side - FR;
+        const bool vk = (vis >> k) & 1;
+        X = vk ? cx : 0; Y = vk ? cy : 0; T = wt[k * kFitQS];
+    };
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t X, Y; uint32_t T;
+        cell(k, X, Y, T);
+        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+    }
+    sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
+    syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
+    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
+                         (double)sy,  (double)sx,  (double)sy, (double)np};
+    double DET = det3_partialpivlu(a);
+    if (DET < 1) return;  // 0 inliers; uniform over the quad
+    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
+    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
+    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
+    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
+    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
+    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);  // (d2, d5, d8: the intercept row, never used)
+    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
+    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
+    const double cz = (double)te * kTsToSec;
+    // (A2 * At) * Y in the reference order (r2, the intercept, is never used:
+    // vFlow.cpp:1352-1377).  Each term m_k * yt_k is one rounded product,
+    // independent of the others, so lane j of the quad forms the terms of
+    // cells k = kb + j, and the sums then add them in order k = 0, 1, ... on
+    // every lane (quad broadcasts): the additions are the reference's, a quarter
+    // of the products per lane.
+    double r0 = 0.0, r1 = 0.0;
+#pragma unroll 1
+    for (int kb = 0; kb < np; kb += 4) {
+        const int k = kb + j < np ? kb + j : np - 1;
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        double m0, m1;
+        if (gemm) {
+            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
+            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
+        } else {
+            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
+            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
+        }
+        const double q0 = m0 * yt, q1 = m1 * yt;
+        const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
+        if (!gemv && kb == 0) { r0 = a0; r1 = a1; }
+        else { r0 = r0 + a0; r1 = r1 + a1; }
+        if (kb + 1 < np) { r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1); }
+        if (kb + 2 < np) { r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1); }
+        if (kb + 3 < np) { r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1); }
+    }
+    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
+    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double ccx = (double)ex, ccy = (double)ey;
+    int inliers = 0;
+#pragma unroll 1
+    for (int k = j; k < np; k += 4) {
+        int64_t Xi, Yi; uint32_t T;
+        cell(k, Xi, Yi, T);
+        const double Tk = (double)T;
+        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+        const double actualdt = yt - cz;
+        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+    }
+    inliers += xch32<0>(inliers);
+    inliers += xch32<1>(inliers);
+    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
+    (void)dtdp;
+    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
+    vy_out = r1;
+    acc_out = true;
+}
+
+// Four lanes per event of chunk [c0, c1) in tile order, the wave's SAE box in
+// LDS (see fit_event_box); lane 0 of the quad stores.
+template <int FR>
+__global__ __launch_bounds__(64) void k_fit_box(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
+    const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
+    if ((int)blockIdx.x >= G) {
+        fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
+                        ((int)blockIdx.x - G) * (int)blockDim.x + (int)threadIdx.x);
+        return;
+    }
+    constexpr int CAP = FitBox<FR>::BOX;
+    __shared__ uint4 s_box[FitBox<FR>::CAP];
+    const int lane = (int)threadIdx.x;
+    const int fb = xcd_block_grouped((int)blockIdx.x, G);
+    const int w = c0 + ((fb * 64 + lane) >> 2);
+    const int j = lane & 3;
+    int4 fd = make_int4(-1, 0, 0, 0);
+    if (w < c1) fd = c.fdesc[w];  // {event, x, y, t}: one 16-B load (k_fit_desc)
+    // halo columns: flows come from their owner (farms_import_flows)
+    const bool active = w < c1 && (c.fit_all || (fd.y >= c.fit_lo && fd.y < c.fit_hi));
+    // ---- the box: bounding box of the union windows of the longest prefix of
+    // the wave's (active) quads that fits CAP cells; wave-uniform scalars
+    const uint64_t act = __ballot(active);
+    int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN, nin = 0;
+    for (int q = 0; q < 16; ++q) {
+        if (!((act >> (4 * q)) & 1)) continue;
+        const int qx = __builtin_amdgcn_readlane(fd.y, 4 * q), qy = __builtin_amdgcn_readlane(fd.z, 4 * q);
+        const int nx0 = min(bx0, qx), nx1 = max(bx1, qx), ny0 = min(by0, qy), ny1 = max(by1, qy);
+        if ((nx1 - nx0 + 1 + 4 * FR) * (ny1 - ny0 + 1 + 4 * FR) > CAP) break;
+        bx0 = nx0; bx1 = nx1; by0 = ny0; by1 = ny1;
+        nin = q + 1;
+    }
+    const int BX0 = bx0 - 2 * FR, BY0 = by0 - 2 * FR;
+    const int BH = nin ? by1 - by0 + 1 + 4 * FR : 1;
+    const int area = nin ? (bx1 - bx0 + 1 + 4 * FR) * BH : 0;
+    {
+        const float inv = 1.0f / (float)BH;
+        for (int idx = lane; idx < area; idx += 64) {
+            int col = (int)((float)idx * inv);  // idx / BH, corrected below (idx < 2^24)
+            if (col * BH > idx) --col;
+            else if ((col + 1) * BH <= idx) ++col;
+            const int u = BX0 + col, v = BY0 + (idx - col * BH);
+            const bool ok = u >= 0 && u < c.W && u >= c.X0 && u < c.XR1 && v >= 0 && v < c.H;
+            const uint4 hd = sae_head(c, ok ? (uint32_t)((u - c.X0) * c.H + v) : 0u);
+            s_box[idx] = ok ? hd : make_uint4(0, 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (!active) return;  // whole quads
+    double vx, vy;
+    bool acc;
+    fit_event_box<FR>(c, fd, seq, j, (lane >> 2) < nin, BX0, BY0, BH, s_box,
+                      reinterpret_cast<uint32_t *>(s_box + CAP) + (lane >> 2), vx, vy, acc);
     if (j == 0) fit_plane(c, fd.x, vx, vy, acc);
 }
 
@@ -2175,19 +2631,19 @@ __global__ void k_seed_sae(Ctx c, const int64_t *stamp) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= c.WH) return;
     const int64_t s = stamp[q + (int64_t)c.X0 * c.H];
-    SaeCell cell{};
-    cell.tag = s >= 0 ? 0x80000000u : 0u;  // chunk seq 0: never matches a chunk
-    cell.tsnap = s >= 0 ? (uint32_t)s : 0u;
-    c.cells[q] = cell;  // both SAE buffers
-    c.cells[q + c.WH] = cell;
+    SaeHead hd{};
+    hd.tag = s >= 0 ? 0x80000000u : 0u;  // chunk seq 0: never matches a chunk
+    hd.tsnap = s >= 0 ? (uint32_t)s : 0u;
+    c.cells.head[q] = hd;  // both SAE buffers (heads are contiguous: buffer 1 follows buffer 0)
+    c.cells.head[q + c.WH] = hd;
 }
 
 // lastEventTime surface for farms_get_last_event_time: stamp of the latest
 // event at each pixel, 0 when never visited (vFlow.cpp:66,264,407).
-__global__ void k_last_time(const SaeCell *cells, int64_t WH, double *out) {
+__global__ void k_last_time(const SaeHead *cells, int64_t WH, double *out) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= WH) return;
-    const SaeCell s = cells[q];
+    const SaeHead s = cells[q];
     out[q] = (s.tag >> 31) ? (double)s.tsnap : 0.0;
 }
 
@@ -2276,7 +2732,8 @@ struct farms_handle {
     int fit_chunk = kDefaultFitChunk, pool_chunk = kDefaultPoolChunk;
     hipStream_t stream = nullptr;
     // persistent surfaces (x-major, W*H cells)
-    SaeCell *cells = nullptr;
+    SaeHead *sae_head = nullptr;  // two buffers of WH heads (fit-chunk parity), then
+    SaeTail *sae_tail = nullptr;  // two of WH tails
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1), indexed by
@@ -2490,7 +2947,8 @@ int reset_surfaces(farms_handle *h) {
     int rc = sync_all(h);
     if (rc) return rc;
     // tag 0: never visited, never touched (chunk seqs start at 1)
-    HIPCHK(hipMemsetAsync(h->cells, 0, 2 * sizeof(SaeCell) * h->WH, h->stream));  // both SAE buffers
+    HIPCHK(hipMemsetAsync(h->sae_head, 0, 2 * sizeof(SaeHead) * h->WH, h->stream));  // both SAE buffers
+    HIPCHK(hipMemsetAsync(h->sae_tail, 0, 2 * sizeof(SaeTail) * h->WH, h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
     for (Work &w : h->ws) {
@@ -2537,22 +2995,23 @@ pool_launcher pool_for(int K, int fr) {
 
 // Fit of chunk [c0, c1); pr.blocks > 0: with the next chunk's prep riding on
 // the same launch (quad path only; returns false when it did not take it).
-bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, bool union_tile,
+bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, int mode,
                 FitPrep pr) {
     if (quad) {
         const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks), b(64);
+#define FARMS_FIT_CASE(FR_)                                                                            \
+    if (mode == 3) hipLaunchKernelGGL((k_fit_box<FR_>), g, b, 0, s, c, c0, c1, seq, pr);              \
+    else if (mode == 2) hipLaunchKernelGGL((k_fit_quad<FR_, 2>), g, b, 0, s, c, c0, c1, seq, pr);     \
+    else if (mode == 1) hipLaunchKernelGGL((k_fit_quad<FR_, 1>), g, b, 0, s, c, c0, c1, seq, pr);     \
+    else hipLaunchKernelGGL((k_fit_quad<FR_, 0>), g, b, 0, s, c, c0, c1, seq, pr);                    \
+    return true;
         switch (fr) {
-        case 1: hipLaunchKernelGGL((k_fit_quad<1, true>), g, b, 0, s, c, c0, c1, seq, pr); return true;
-        case 2:
-            if (union_tile) hipLaunchKernelGGL((k_fit_quad<2, true>), g, b, 0, s, c, c0, c1, seq, pr);
-            else hipLaunchKernelGGL((k_fit_quad<2, false>), g, b, 0, s, c, c0, c1, seq, pr);
-            return true;
-        case 3:
-            if (union_tile) hipLaunchKernelGGL((k_fit_quad<3, true>), g, b, 0, s, c, c0, c1, seq, pr);
-            else hipLaunchKernelGGL((k_fit_quad<3, false>), g, b, 0, s, c, c0, c1, seq, pr);
-            return true;
+        case 1: FARMS_FIT_CASE(1)
+        case 2: FARMS_FIT_CASE(2)
+        case 3: FARMS_FIT_CASE(3)
         default: return false;
         }
+#undef FARMS_FIT_CASE
     }
     const dim3 g(ceil_div(c1 - c0, 256)), b(256);
     switch (fr) {
@@ -2602,7 +3061,7 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = w.pix; c.skey = w.skey; c.P = w.P; c.link = w.link;
     c.Q = w.Q; c.qe = w.qe; c.fdesc = w.fdesc; c.plane = w.plane;
-    c.cells = h->cells; c.PT = w.PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
+    c.cells = SaeBuf{h->sae_head, h->sae_tail}; c.PT = w.PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
     c.pcur = w.pcur; c.pend = w.pend;
     c.serial = h->prm.serial != 0;
@@ -2731,8 +3190,11 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
     const bool fit_quad = !(fq && fq[0] == '0');
-    const char *fu = getenv("FARMS_FIT_UNION");  // A/B aid: 0 = re-gather the winning window
-    const bool fit_ut = !(fu && fu[0] == '0');
+    // A/B aid: FARMS_FIT_MODE 0 = re-gather the winning window, 1 = union tile
+    // with columns per lane, 2 = union tile with rows per lane, 3 = the wave's
+    // SAE box in LDS (default)
+    const char *fu = getenv("FARMS_FIT_MODE");
+    const int fit_mode = fu ? atoi(fu) : 3;
     int fit_launches = 0;
     auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
     // The SAE is double-buffered by chunk parity (buffer f % 2 serves chunk f),
@@ -2740,7 +3202,10 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     // chunk.  Chunk seqs are base + f + 1.
     const uint32_t seq_base = h->seq;
     h->seq += (uint32_t)n_fit_chunks;
-    auto cells_of = [&](int f) { return h->cells + (size_t)(f & 1) * (size_t)h->WH; };
+    auto cells_of = [&](int f) {
+        const size_t o = (size_t)(f & 1) * (size_t)h->WH;
+        return SaeBuf{h->sae_head + o, h->sae_tail + o};
+    };
     auto fit_start = [&](int f) { return f * h->fit_chunk; };
     auto prep_of = [&](int f) {  // the prep of chunk f (into buffer f % 2); blocks for 64-thread blocks
         FitPrep pr{cells_of(f), fit_start(std::max(f - 2, 0)), fit_start(f), fit_chunk_end(f), seq_base + f + 1, 0};
@@ -2761,7 +3226,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (prof && h->fit_events) { int rc = mark(h, s, &k0); if (rc) return rc; }
         bool merged = false;
         if (fast_fit) {
-            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_ut, next);
+            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_mode, next);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
             hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, w.Q + c0,
                                c1 - c0);
@@ -3046,7 +3511,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
                 return bail(fail(FARMS_EHIP, "hipEventCreate"));
     }
-    if ((rc = dalloc(&h->cells, 2 * h->WH)) || (rc = dalloc(&h->ftime, h->WH)) ||
+    if ((rc = dalloc(&h->sae_head, 2 * h->WH)) || (rc = dalloc(&h->sae_tail, 2 * h->WH)) ||
+        (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
         (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 2)) || (rc = dalloc(&h->counters, 8)))
@@ -3064,7 +3530,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     if (h->s_copy) (void)hipStreamSynchronize(h->s_copy);
-    dfree(h->cells); dfree(h->ftime); dfree(h->fsnap);
+    dfree(h->sae_head); dfree(h->sae_tail); dfree(h->ftime); dfree(h->fsnap);
     for (Work &w : h->ws) {
         free_workspace(w);
         dfree(w.pcur); dfree(w.pend);
@@ -3132,7 +3598,7 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     HIPCHK(hipSetDevice(h->prm.device));
     double *d = nullptr;
     HIPCHK(hipMalloc((void **)&d, sizeof(double) * h->WH));
-    hipLaunchKernelGGL(k_last_time, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, h->cells, h->WH, d);
+    hipLaunchKernelGGL(k_last_time, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, h->sae_head, h->WH, d);
     for (int64_t q = 0; q < (int64_t)h->W * h->H; ++q) out[q] = 0.0;  // columns outside the region
     hipError_t err = hipMemcpyAsync(out + (int64_t)h->X0 * h->H, d, sizeof(double) * h->WH, hipMemcpyDeviceToHost,
                                     h->stream);
@@ -3142,8 +3608,8 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     // (vFlow.cpp:556); it shows until an event fires at that pixel (which marks
     // the pixel's SAE cell visited)
     if (err == hipSuccess && h->first_q >= 0) {
-        SaeCell cell{};
-        err = hipMemcpy(&cell, h->cells + (h->first_q - (int64_t)h->X0 * h->H), sizeof(cell), hipMemcpyDeviceToHost);
+        SaeHead cell{};
+        err = hipMemcpy(&cell, h->sae_head + (h->first_q - (int64_t)h->X0 * h->H), sizeof(cell), hipMemcpyDeviceToHost);
         if (err == hipSuccess && !(cell.tag >> 31)) out[h->first_q] = (double)h->first_t;
     }
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
@@ -3188,7 +3654,7 @@ extern "C" int farms_seed_sae(farms_handle *h, const int64_t *d_stamp) {
     if (!h || !d_stamp) return fail(FARMS_EINVAL, "null argument");
     HIPCHK(hipSetDevice(h->prm.device));
     Ctx c{};
-    c.W = h->W; c.H = h->H; c.WH = h->WH; c.X0 = h->X0; c.cells = h->cells;
+    c.W = h->W; c.H = h->H; c.WH = h->WH; c.X0 = h->X0; c.cells = SaeBuf{h->sae_head, h->sae_tail};
     hipLaunchKernelGGL(k_seed_sae, dim3(ceil_div(h->WH, 256)), dim3(256), 0, h->stream, c, d_stamp);
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());

@@ -256,14 +256,16 @@ def test_out_of_sensor_event_is_rejected():
 
 @pytest.mark.parametrize("fs", [3, 5, 7])
 def test_fit_variants_are_bitwise_identical(fs, monkeypatch):
-    """The quad-lane fit (with and without the union tile) and the one-thread
-    fit evaluate the same arithmetic in the same order: bitwise-equal records."""
+    """The quad-lane fits (FARMS_FIT_MODE 0: re-gathered winning window, 1:
+    union tile by columns, 2: union tile by rows, 3: the wave's SAE box in LDS)
+    and the one-thread fit evaluate the same arithmetic in the same order:
+    bitwise-equal records."""
     ev = farms.synth_config(3, 150_000)
     x, y, t, p = ev.relative()
     outs = []
-    for quad, union in [("1", "1"), ("1", "0"), ("0", "1")]:
+    for quad, mode in [("1", "3"), ("1", "0"), ("1", "1"), ("1", "2"), ("0", "3")]:
         monkeypatch.setenv("FARMS_FIT_QUAD", quad)
-        monkeypatch.setenv("FARMS_FIT_UNION", union)
+        monkeypatch.setenv("FARMS_FIT_MODE", mode)
         with farms.FlowManager(720, 1280, fs, 5) as fm:
             outs.append(fm.process(x, y, t, p))
     for o in outs[1:]:

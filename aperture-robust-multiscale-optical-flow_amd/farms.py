@@ -25,6 +25,7 @@ FARMS_EINVAL = -1
 FARMS_EHIP = -2
 FARMS_ENOMEM = -3
 FARMS_ENODEV = -4
+FARMS_EINTERNAL = -5
 PROF_TIMING = 1    # farms_set_profiling: HIP events around phases and k_fit / k_pool launches
 PROF_COUNTERS = 2  # ... plus the U_loc / U_pool / candidate / contributor counters
 PROF_POOL = 3      # HIP events around phases and k_pool launches only

@@ -29,6 +29,7 @@ extern "C" {
 #define FARMS_EHIP (-2)    /* a HIP runtime call failed (message in farms_last_error) */
 #define FARMS_ENOMEM (-3)  /* device or host allocation failed */
 #define FARMS_ENODEV (-4)  /* no usable gfx950 device */
+#define FARMS_EINTERNAL (-5) /* an internal ordering invariant of the engine failed (a bug; message in farms_last_error) */
 
 typedef struct farms_handle farms_handle;
 

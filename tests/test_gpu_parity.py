@@ -147,17 +147,21 @@ def test_chunking_is_bitwise_invariant():
         assert bitwise_equal(outs[0], o)
 
 
-def test_pool_occupancy_cap_is_bitwise_invariant(monkeypatch):
-    """k_pool is built twice (7- and 6-wave VGPR floors, pool_for picks by
-    filter size): both builds give the same bits."""
+def test_pool_variants_are_bitwise_invariant(monkeypatch):
+    """k_pool is built four ways (7- and 6-wave VGPR floors, pool_for picks by
+    filter size; group pooling -- one wave per (chunk, tile) group with the
+    union window's headers in LDS -- or one wave per event,
+    FARMS_POOL_GROUP=0): every build gives the same bits."""
     ev = farms.synth_config(3, 120_000)
     x, y, t, p = ev.relative()
     outs = []
-    for cap in ("7", "6"):
+    for cap, grp in (("7", "1"), ("6", "1"), ("7", "0"), ("6", "0")):
         monkeypatch.setenv("FARMS_POOL_CAP", cap)
+        monkeypatch.setenv("FARMS_POOL_GROUP", grp)
         with farms.FlowManager(720, 1280, 5, 5) as fm:
             outs.append(fm.process(x, y, t, p))
-    assert bitwise_equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert bitwise_equal(outs[0], o)
 
 
 def test_streaming_split_equals_one_call():
@@ -257,13 +261,14 @@ def test_out_of_sensor_event_is_rejected():
 @pytest.mark.parametrize("fs", [3, 5, 7])
 def test_fit_variants_are_bitwise_identical(fs, monkeypatch):
     """The quad-lane fits (FARMS_FIT_MODE 0: re-gathered winning window, 1:
-    union tile by columns, 2: union tile by rows, 3: the wave's SAE box in LDS)
+    union tile by columns, 2: union tile by rows, 3: the wave's SAE box in LDS,
+    4: the box scan ending at the winning window, then one lane per event)
     and the one-thread fit evaluate the same arithmetic in the same order:
     bitwise-equal records."""
     ev = farms.synth_config(3, 150_000)
     x, y, t, p = ev.relative()
     outs = []
-    for quad, mode in [("1", "3"), ("1", "0"), ("1", "1"), ("1", "2"), ("0", "3")]:
+    for quad, mode in [("1", "3"), ("1", "0"), ("1", "1"), ("1", "2"), ("1", "4"), ("0", "3")]:
         monkeypatch.setenv("FARMS_FIT_QUAD", quad)
         monkeypatch.setenv("FARMS_FIT_MODE", mode)
         with farms.FlowManager(720, 1280, fs, 5) as fm:
@@ -345,6 +350,29 @@ def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
     dd.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
     assert bitwise_equal(g, dd)
     assert g1.n == 777 and np.array_equal(g1.scale, dd["scale"][:777])
+
+
+@pytest.mark.parametrize("subs,echo", [("1", "1"), ("3", "0"), ("16", "1")])
+def test_host_path_pipeline_knobs_are_bitwise_invariant(subs, echo, monkeypatch):
+    """The host path's pipeline knobs change only how the work is cut and
+    moved: FARMS_SUBBATCHES (one call, or n/k events per sub-batch) and
+    FARMS_ECHO_DMA=0 (the x/y/t/p echo into pinned record columns by host
+    copies instead of D2H) give bitwise the default's records."""
+    ev = farms.synth_config(3, 2_000_000)
+    x, y, t, p = ev.relative()
+    keep = []
+    ins = [x, y, t, p]
+    for i in range(4):
+        ins[i], own = farms.pinned(ins[i])
+        keep.append(own)
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
+        ref = fm.process(*ins, out=farms.Records(len(x), pinned=True))
+    monkeypatch.setenv("FARMS_SUBBATCHES", subs)
+    monkeypatch.setenv("FARMS_ECHO_DMA", echo)
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
+        g = fm.process(*ins, out=farms.Records(len(x), pinned=True))
+    assert bitwise_equal(ref, g)
+    assert np.array_equal(g.x, x) and np.array_equal(g.t.view(np.uint32), t)
 
 
 @pytest.mark.parametrize("pin", [False, True])

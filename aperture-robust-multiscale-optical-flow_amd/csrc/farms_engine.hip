@@ -3291,10 +3291,34 @@ pool_launcher pool_for_cap(int K) {
 // k_pool's occupancy cap by the fit's weight (see k_pool): 7 waves per SIMD
 // beside the fs <= 5 fits, 6 beside the heavier fs-7 and wave fits;
 // FARMS_POOL_CAP=6|7 overrides (tuning aid).
-pool_launcher pool_for(int K, int fr) {
+bool pool_w7(int fr) {
     bool w7 = fr <= 2;
     if (const char *v = getenv("FARMS_POOL_CAP")) w7 = v[0] == '7';
-    return w7 ? pool_for_cap<true>(K) : pool_for_cap<false>(K);
+    return w7;
+}
+pool_launcher pool_for(int K, int fr) {
+    return pool_w7(fr) ? pool_for_cap<true>(K) : pool_for_cap<false>(K);
+}
+// Tuning knobs of the fit (A/B aids; every choice gives the same bits):
+// FARMS_FIT_QUAD=0: one thread per event; FARMS_FIT_MODE 0 = re-gather the
+// winning window, 1 = union tile with columns per lane, 2 = union tile with
+// rows per lane, 3 = the wave's SAE box in LDS (default), 4 = the box scan
+// ending at the winning window, then one lane per event for the solve
+// (fit_solve, riding on the next chunk's fit launch).
+bool fit_quad_env() {
+    const char *fq = getenv("FARMS_FIT_QUAD");
+    return !(fq && fq[0] == '0');
+}
+int fit_mode_env() {
+    const char *fu = getenv("FARMS_FIT_MODE");
+    const int m = fu ? atoi(fu) : 3;
+    return m >= 0 && m <= 4 ? m : 3;
+}
+// Group pooling (FARMS_POOL_GROUP=0: one wave per event) for windows whose
+// union over a work-order tile fits the 128-row table.
+bool pool_group_on(const farms_handle *h) {
+    const char *pg = getenv("FARMS_POOL_GROUP");
+    return !(pg && pg[0] == '0') && 2 * h->M + (1 << h->tile_shift) <= 128;
 }
 
 // FARMS_FIT_MODE 4: the solve of fit-chunk positions [s0, s1) on its own.
@@ -3387,9 +3411,8 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.ring0 = (int)(h->chunk_base % h->NB);
     // group pooling (FARMS_POOL_GROUP=0: one wave per event; A/B aid), for
     // windows whose union over a work-order tile fits the 128-row table
-    const char *pg = getenv("FARMS_POOL_GROUP");
     const int tile = 1 << h->tile_shift;
-    const bool group = !(pg && pg[0] == '0') && 2 * h->M + tile <= 128;
+    const bool group = pool_group_on(h);
     c.gkey = w.wkey_sorted;
     c.pool_capg = group ? kPoolGroupCap : 0;
     // pooling window rows and columns (group: of the union of a tile's windows)
@@ -3536,15 +3559,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
     pool_launcher pl = pool_for(h->K, h->fr);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
-    const char *fq = getenv("FARMS_FIT_QUAD");  // A/B aid: 0 = one thread per event
-    const bool fit_quad = !(fq && fq[0] == '0');
-    // A/B aid: FARMS_FIT_MODE 0 = re-gather the winning window, 1 = union tile
-    // with columns per lane, 2 = union tile with rows per lane, 3 = the wave's
-    // SAE box in LDS (default), 4 = the box scan ending at the winning window,
-    // then one lane per event for the solve (k_fit_solve's arithmetic, riding
-    // on the next chunk's fit launch)
-    const char *fu = getenv("FARMS_FIT_MODE");
-    const int fit_mode = fu ? atoi(fu) : 3;
+    const bool fit_quad = fit_quad_env();
+    const int fit_mode = fit_mode_env();
     const bool split = fast_fit && fit_quad && fit_mode == 4;
     if (split && !h->fwin) {  // two chunks' window records (the scanned chunk and the one being solved)
         const int np = (2 * h->fr + 1) * (2 * h->fr + 1);
@@ -3975,6 +3991,25 @@ extern "C" int farms_get_stats(const farms_handle *h, farms_stats *out) {
 }
 
 extern "C" int farms_num_scales(const farms_handle *h) { return h ? h->K : 0; }
+
+extern "C" int farms_kernel_info(const farms_handle *h, char *buf, int32_t len) {
+    if (!h || !buf || len <= 0) return fail(FARMS_EINVAL, "null argument");
+    const bool fast = h->fr >= 1 && h->fr <= 3, quad = fit_quad_env();
+    const int mode = fit_mode_env();
+    const std::string fr = std::to_string(h->fr);
+    std::string fit, solve;
+    if (!fast) fit = "k_fit_wave";
+    else if (!quad) fit = "k_fit<" + fr + ">";
+    else if (mode >= 3) fit = "k_fit_box<" + fr + ">";
+    else fit = "k_fit_quad<" + fr + ">";
+    if (fast && quad && mode == 4) solve = "k_fit_box<" + fr + ">+k_fit_solve<" + fr + ">";
+    const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(quad ? mode : -1) +
+                           ", \"fit_solve\": \"" + solve + "\", \"pool\": \"k_pool<" + std::to_string(h->K) +
+                           ">\", \"pool_group\": " + (pool_group_on(h) ? "1" : "0") +
+                           ", \"pool_cap\": " + (pool_w7(h->fr) ? "7" : "6") + "}";
+    std::snprintf(buf, (size_t)len, "%s", js.c_str());
+    return FARMS_OK;
+}
 
 extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");

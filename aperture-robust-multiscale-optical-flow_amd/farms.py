@@ -115,7 +115,7 @@ HIP_SYMBOLS = (
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
     "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
     "farms_seed_sae", "farms_serial_first", "farms_fit_device", "farms_pool_device", "farms_export_flows",
-    "farms_import_flows", "farms_host_alloc", "farms_host_free",
+    "farms_import_flows", "farms_host_alloc", "farms_host_free", "farms_kernel_info",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text",
                  "farms_synth_generate_select", "farms_synth_column_hist")
@@ -410,6 +410,15 @@ class FlowManager:
     @property
     def num_scales(self) -> int:
         return int(self._lib.farms_num_scales(self._h))
+
+    def kernel_info(self) -> dict:
+        """The kernels the next call runs (farms_kernel_info), e.g.
+        {"fit": "k_fit_box<2>", "pool": "k_pool<11>", ...}."""
+        import json
+
+        buf = ctypes.create_string_buffer(512)
+        _check(self._lib, self._lib.farms_kernel_info(self._h, buf, ctypes.c_int32(512)))
+        return json.loads(buf.value.decode())
 
     def reset(self) -> None:
         _check(self._lib, self._lib.farms_reset(self._h))

@@ -205,11 +205,12 @@ def kernel_roofline(cfg: int, split: str, kernel: str, kname: str, launches: int
     return r
 
 
-def rooflines(cfg: int, split: str, ts: dict, cs: dict) -> dict:
+def rooflines(cfg: int, split: str, ts: dict, cs: dict, ki: dict) -> dict:
     """Both hot kernels' rooflines from the timed steps' stats `ts` (HIP-event
     launch brackets) and the counted step's `cs`, keyed "k_fit" / "k_pool";
     "dominant" names the one with more kernel time per step (the pooling at
-    filtersize 5, the fit at filtersize 7)."""
+    filtersize 5, the fit at filtersize 7).  `ki` names the kernels the engine
+    ran (farms_kernel_info), as the PMC summaries key them."""
     fs = FILTER[cfg]
     jump, maxw = scales(cfg)
     nf, npl = max(ts["fit_launches"], 1), max(ts["pool_launches"], 1)
@@ -220,14 +221,17 @@ def rooflines(cfg: int, split: str, ts: dict, cs: dict) -> dict:
     # writes the 52-B record
     fit_algo = (4.0 * cs["sae_cells"] + 33.0 * cs["n_events"]) / nf
     pool_algo = (20.0 * cs["pool_cells"] + 52.0 * owned) / npl
+    fit_k = ki.get("fit", f"k_fit_quad<{fs // 2}>")
+    pool_k = ki.get("pool", f"k_pool<{maxw // jump + 1}>")
     out = {
-        "k_fit": kernel_roofline(cfg, split, "k_fit_quad", f"k_fit_quad<{fs // 2}>", ts["fit_launches"],
+        "k_fit": kernel_roofline(cfg, split, fit_k.split("<")[0], fit_k, ts["fit_launches"],
                                  ts["ms_fit_kernel"] * 1e3 / nf, fit_algo,
                                  "latency (dependent L2 loads of the SAE union window), not HBM: see issue"),
-        "k_pool": kernel_roofline(cfg, split, "k_pool", f"k_pool<{maxw // jump + 1}>", ts["pool_launches"],
+        "k_pool": kernel_roofline(cfg, split, pool_k.split("<")[0], pool_k, ts["pool_launches"],
                                   ts["ms_pool_kernel"] * 1e3 / npl, pool_algo,
                                   "latency (dependent L2 loads and the fp64 fold chain), not HBM: see issue"),
     }
+    out["kernels"] = ki
     out["dominant"] = "k_fit" if ts["ms_fit_kernel"] > ts["ms_pool_kernel"] else "k_pool"
     return out
 
@@ -421,7 +425,7 @@ def main():
     fm.set_profiling(True)
     st.step()
     cs = fm.stats()
-    rl = rooflines(cfg, args.split, ts, cs)
+    rl = rooflines(cfg, args.split, ts, cs, fm.kernel_info())
     dom = rl["dominant"]
     mine = {"rank": rank, "ms_step_rank": round(elapsed_rank / args.steps * 1e3, 3),
             "stored_events": n, "owned_events": n_owned,
@@ -443,6 +447,7 @@ def main():
     roofline["other"] = {k: {f: rl[k].get(f) for f in ("kernel", "frac", "achieved", "avg_launch_us",
                                                         "launches_per_step", "traffic_source")}
                          for k in ("k_fit", "k_pool") if k != dom}
+    roofline["engine_kernels"] = rl["kernels"]
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mevents/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,

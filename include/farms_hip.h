@@ -202,6 +202,13 @@ int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_t t_abs);
 /* Number of pooling scales, floor(max_window / window_jump) + 1. */
 int farms_num_scales(const farms_handle *h);
 
+/* The kernels the handle's next call runs (its filter and scales, and the
+ * FARMS_FIT_* / FARMS_POOL_* tuning knobs as they are now), as a JSON object
+ * in buf (NUL-terminated, truncated to len): {"fit": "k_fit_box<2>",
+ * "fit_mode": 3, "fit_solve": "", "pool": "k_pool<11>", "pool_group": 1,
+ * "pool_cap": 7}.  Not in the reference (measurement aid for bench.py). */
+int farms_kernel_info(const farms_handle *h, char *buf, int32_t len);
+
 /* Thread-local message for the last non-OK status. */
 const char *farms_last_error(void);
 

@@ -87,12 +87,13 @@ def test_rooflines_name_the_dominant_kernel_per_config():
 
     ts = {"fit_launches": 100, "pool_launches": 10, "ms_fit_kernel": 50.0, "ms_pool_kernel": 20.0}
     cs = {"n_events": 1000, "n_owned": 1000, "n_valid": 400, "sae_cells": 169e3, "pool_cells": 4e6}
-    rl = bench.rooflines(4, "segments", ts, cs)
-    assert rl["dominant"] == "k_fit"
+    ki = {"fit": "k_fit_box<3>", "pool": "k_pool<11>"}  # farms_kernel_info's names
+    rl = bench.rooflines(4, "segments", ts, cs, ki)
+    assert rl["dominant"] == "k_fit" and rl["k_fit"]["kernel"] == "k_fit_box"
     assert rl["k_fit"]["avg_launch_us"] == 500.0 and rl["k_pool"]["avg_launch_us"] == 2000.0
     assert rl["k_fit"]["algorithmic_bytes_per_launch"] == round((4 * 169e3 + 33 * 1000) / 100)
     ts.update(ms_fit_kernel=10.0)
-    rl = bench.rooflines(3, "segments", ts, cs)
+    rl = bench.rooflines(3, "segments", ts, cs, dict(ki, fit="k_fit_box<2>"))
     assert rl["dominant"] == "k_pool"
     for k in ("k_fit", "k_pool"):
         r = rl[k]

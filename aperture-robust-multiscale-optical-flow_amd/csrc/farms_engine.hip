@@ -159,10 +159,6 @@ constexpr int kPoolHalves = 1;
 // k_pool staging: {L, L cos, L sin, 1} and k0 of the 64 x kPoolHalves entries of a step, 8-B words
 constexpr int kPoolValWords = (4 * 64 + 8) * kPoolHalves;
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
-constexpr int kLeadBit = 1 << 30;  // qe[w].y: first work-order position of its (chunk, tile) group
-// group pooling: candidate headers of a group's union window staged in LDS
-// per wave (16 B + 4 B each); a larger union pools its events one by one
-constexpr int kPoolGroupCap = 512;
 
 struct Ctx {
     int W, H, n;
@@ -179,13 +175,8 @@ struct Ctx {
     const uint32_t *pix;   // x*H + y per event
     const uint32_t *skey;  // pixel ids, sorted
     const int32_t *P;      // event ids sorted by (pixel, id)
-    uint32_t *fwin;        // FARMS_FIT_MODE 4: the fit chunk's window records (rows of fws words)
-    int fws;
     const int32_t *Q;      // event ids ordered by (pooling chunk, 8x8 tile): work order
-    const uint32_t *gkey;  // per work-order position: its (pooling chunk, tile) key, sorted
-    // per work-order position: {event id or -1 if not pooled, x | kLeadBit on
-    // the first position of its (chunk, tile) group, y, t} (k_pool_desc)
-    int4 *qe;
+    int4 *qe;              // per work-order position: {event id or -1 if not pooled, x, y, t} (k_pool_desc)
     int4 *fdesc;           // per work-order position: {event id, x, y, t} (k_fit_desc)
     // per event, one 16-B record (k_link): {position in P, previous and next
     // event at the pixel (-1 / INT_MAX: none), tpv}; tpv = the stamp the
@@ -211,7 +202,6 @@ struct Ctx {
     int NB, C2;            // ring size, events per pooling chunk
     int ring0;             // ring buffer of the call's first pooling chunk (chunk numbers continue across calls)
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
-    int pool_capg;         // group pooling: candidate headers a wave stages in LDS (0: one wave per event)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
     // with its pixel's lastEventTime still holding link.w, the stamp before it
@@ -427,10 +417,7 @@ __global__ void k_pool_desc(Ctx c, int p0, int p1) {
     if (w >= p1) return;
     const int4 fd = c.fdesc[w];
     const bool ok = c.valid[fd.x] && fd.y >= c.own_lo && fd.y < c.own_hi;
-    // the first position of each (chunk, tile) group carries kLeadBit in x:
-    // group pooling (k_pool<K, W7, true>) runs one wave per group
-    const bool lead = w == 0 || c.gkey[w] != c.gkey[w - 1];
-    c.qe[w] = make_int4(ok ? fd.x : -1, fd.y | (lead ? kLeadBit : 0), fd.z, fd.w);
+    c.qe[w] = make_int4(ok ? fd.x : -1, fd.y, fd.z, fd.w);
 }
 
 // Fit descriptor per work-order position: {event, x, y, t}, so that a fit
@@ -459,19 +446,7 @@ struct FitPrep {
     int p0, c0, c1;
     uint32_t seq;
     int blocks;  // prep blocks after the fit's
-    // FARMS_FIT_MODE 4: the solve of the previous fit chunk's positions
-    // [s0, s1) rides on the launch too, in sblocks one-wave blocks between the
-    // fit's and the prep's, from that chunk's windows (fw, rows of fws words)
-    int s0, s1, sblocks;
-    const uint32_t *fw;
-    int fws;
 };
-// FARMS_FIT_MODE 4 window records (k_fit_box<FR, true> -> k_fit_solve): per
-// fit-chunk position p, rows of fws words: [0] / [1] the low / high half of a
-// 64-bit meta word (visited bits of the np cells, the winning window's index
-// at kWinShift, kWinFound), [2 + k] the stamp of window cell k (cx-major).
-constexpr int kWinShift = 56;
-constexpr uint64_t kWinFound = 1ull << 63;
 
 // ---------------------------------------------------------------------------
 // Eigen 3.4 PartialPivLU<MatrixXd>::determinant() of the 3x3 normal matrix
@@ -1528,373 +1503,6 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// Box variant (MODE 3): the 16 events of a fit wave are neighbours in tile
-// order, so their union windows overlap.  The wave loads the SAE heads of the
-// bounding box of its events' union windows into LDS once (consecutive lanes
-// read consecutive rows of a column: consecutive x-major cells), and every
-// quad resolves its cells from there instead of issuing its own global loads
-// (81 / 169 per event at filter 5 / 7).  Events past the box's capacity (the
-// greedy prefix of the wave's quads whose bounding box fits) read the global
-// heads as before.  The box holds heads only: "as of e" is resolved per event
-// (sae_resolve_h, whose rare second-event lookups read the tail array).
-// Scores are exact int64 sums in any order; the winning window is resolved
-// again by each lane for its own cells k = j, j + 4, ... (registers), which is
-// what the AtA sums, the ordered (A2 * At) * Y terms and the inlier test read
-// (a window tile of np x 16 stamps past the box; no union tile).
-template <int FR> struct FitBox {
-    static constexpr int CAP = FR == 1 ? 320 : FR == 2 ? 576 : 768;  // 16-B LDS slots per wave
-    static constexpr int WT = ((2 * FR + 1) * (2 * FR + 1) * kFitQS + 3) / 4;  // of them for the window tile
-    static constexpr int BOX = CAP - WT;  // box cells
-};
-
-// SPLIT (FARMS_FIT_MODE 4): the function ends at the winning window -- the
-// quad's lanes store its stamps (cell k at fw[(2 + k) * fws]) and `meta` gets
-// the visited bits, the window index and kWinFound -- and k_fit_solve, one
-// lane per event, runs the rest (fit_solve).
-template <int FR, bool SPLIT = false>
-__device__ __forceinline__ void fit_event_box(const Ctx &c, int4 fd, uint32_t seq, int j, bool inbox, int BX0, int BY0,
-                                              int BH, const uint4 *box, uint32_t *wt, double &vx_out, double &vy_out,
-                                              bool &acc_out, uint32_t *fw = nullptr, int fws = 0,
-                                              uint64_t *meta = nullptr) {
-    constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
-    constexpr int NR = (US + 3) / 4;   // union rows per lane
-    const int W = c.W, H = c.H;
-    const int e = fd.x, ex = fd.y, ey = fd.z;
-    const uint32_t te = (uint32_t)fd.w;
-    vx_out = 0.0;
-    vy_out = 0.0;
-    acc_out = false;
-    if constexpr (SPLIT) *meta = 0;
-    bool wok[9];
-    int64_t score[9];
-    bool any = false;
-#pragma unroll
-    for (int w = 0; w < 9; ++w) {
-        const int ci = ex + (w / 3 - 1) * FR, cj = ey + (w % 3 - 1) * FR;
-        wok[w] = ci - FR >= 0 && ci + FR <= W - 1 && cj - FR >= 0 && cj + FR <= H - 1;
-        score[w] = 0;
-        any |= wok[w];
-    }
-    if (!any) return;  // uniform over the quad
-    // head of cell (u, v), zero outside the sensor / the stored region: from
-    // the box, or (events past its capacity) from global memory, an
-    // unconditional load from a clamped index
-    auto head_at = [&](int u, int v) -> uint4 {
-        const bool ok = u >= 0 && u < W && u >= c.X0 && u < c.XR1 && v >= 0 && v < H;
-        uint4 hd;
-        if (inbox) hd = box[(u - BX0) * BH + (v - BY0)];
-        else hd = sae_head(c, ok ? (uint32_t)((u - c.X0) * H + v) : 0u);
-        return ok ? hd : make_uint4(0, 0, 0, 0);
-    };
-    // ---- window scores (vFlow.cpp:870-912): this lane's union rows j, j + 4, ...
-    const int v0 = ey - 2 * FR;
-#pragma unroll 1
-    for (int ucol = 0; ucol < US; ++ucol) {
-        const int u = ex + ucol - 2 * FR;
-        uint4 hc[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int i = j + 4 * r;
-            hc[r] = head_at(u, i < US ? v0 + i : -1);
-        }
-        if (u < 0 || u >= W) continue;
-        int64_t sv[3] = {0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int i = j + 4 * r, v = v0 + i;
-            if (i >= US || v < 0 || v >= H) continue;
-            const int64_t st = sae_resolve_h(c, hc[r], (uint32_t)((u - c.X0) * H + v), e, seq);
-            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-            const int64_t d = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
-#pragma unroll
-            for (int ovi = 0; ovi < 3; ++ovi)
-                if (i >= ovi * FR && i <= ovi * FR + 2 * FR) sv[ovi] += d;
-        }
-        const int du = ucol - 2 * FR;
-#pragma unroll
-        for (int oui = 0; oui < 3; ++oui) {
-            const int ou = (oui - 1) * FR;
-            if (du - ou <= FR && ou - du <= FR) {
-#pragma unroll
-                for (int ovi = 0; ovi < 3; ++ovi) score[oui * 3 + ovi] += sv[ovi];
-            }
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < 9; ++w) score[w] = quad_sum_i64(score[w]);
-    const int64_t nn = np;
-    int64_t best = nn * ((int64_t(1) << 32) + 1);  // MAXSTAMP + 1 per cell
-    int bw = -1;
-#pragma unroll
-    for (int w = 0; w < 9; ++w)
-        if (wok[w] && score[w] < best) { best = score[w]; bw = w; }
-    if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
-
-    // ---- the winning window, cx-major (vFlow.cpp:923-930): this lane resolves
-    // its cells k = j, j + 4, ... into the quad's window tile wt (stride 16,
-    // past the box) and their visited bits, combined over the quad
-    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
-    uint64_t vis = 0;
-#pragma unroll 1
-    for (int k = j; k < np; k += 4) {
-        const int u = bi + k / side - FR, v = bj + k % side - FR;
-        const int64_t st = sae_resolve_h(c, head_at(u, v), (uint32_t)((u - c.X0) * H + v), e, seq);
-        if constexpr (SPLIT) fw[(2 + k) * fws] = st < 0 ? 0u : (uint32_t)st;
-        else wt[k * kFitQS] = st < 0 ? 0u : (uint32_t)st;
-        vis |= st >= 0 ? 1ull << k : 0ull;
-    }
-    vis = quad_or_u64(vis);
-    if constexpr (SPLIT) {
-        *meta = vis | ((uint64_t)bw << kWinShift) | kWinFound;
-        return;
-    }
-    // the window's stamps were written by the other lanes of this wave's quad
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {  // k in the reference order: cx-major
-        const int cx = bi + k / side - FR, cy = bj + k % side - FR;
-        const bool vk = (vis >> k) & 1;
-        X = vk ? cx : 0; Y = vk ? cy : 0; T = wt[k * kFitQS];
-    };
-    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
-#pragma unroll 1
-    for (int k = j; k < np; k += 4) {
-        int64_t X, Y; uint32_t T;
-        cell(k, X, Y, T);
-        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
-    }
-    sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
-    syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
-    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
-                         (double)sy,  (double)sx,  (double)sy, (double)np};
-    double DET = det3_partialpivlu(a);
-    if (DET < 1) return;  // 0 inliers; uniform over the quad
-    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
-    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
-    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
-    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
-    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
-    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);  // (d2, d5, d8: the intercept row, never used)
-    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
-    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
-    const double cz = (double)te * kTsToSec;
-    // (A2 * At) * Y in the reference order (r2, the intercept, is never used:
-    // vFlow.cpp:1352-1377).  Each term m_k * yt_k is one rounded product,
-    // independent of the others, so lane j of the quad forms the terms of
-    // cells k = kb + j, and the sums then add them in order k = 0, 1, ... on
-    // every lane (quad broadcasts): the additions are the reference's, a quarter
-    // of the products per lane.
-    double r0 = 0.0, r1 = 0.0;
-#pragma unroll 1
-    for (int kb = 0; kb < np; kb += 4) {
-        const int k = kb + j < np ? kb + j : np - 1;
-        int64_t Xi, Yi; uint32_t T;
-        cell(k, Xi, Yi, T);
-        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-        double m0, m1;
-        if (gemm) {
-            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
-            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
-        } else {
-            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
-            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
-        }
-        const double q0 = m0 * yt, q1 = m1 * yt;
-        const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
-        if (!gemv && kb == 0) { r0 = a0; r1 = a1; }
-        else { r0 = r0 + a0; r1 = r1 + a1; }
-        if (kb + 1 < np) { r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1); }
-        if (kb + 2 < np) { r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1); }
-        if (kb + 3 < np) { r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1); }
-    }
-    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
-    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
-    const double ccx = (double)ex, ccy = (double)ey;
-    int inliers = 0;
-#pragma unroll 1
-    for (int k = j; k < np; k += 4) {
-        int64_t Xi, Yi; uint32_t T;
-        cell(k, Xi, Yi, T);
-        const double Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
-        const double actualdt = yt - cz;
-        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
-    }
-    inliers += xch32<0>(inliers);
-    inliers += xch32<1>(inliers);
-    if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    (void)dtdp;
-    vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
-    vy_out = r1;
-    acc_out = true;
-}
-
-// The rest of the fit of work-order position w from its window record (fw,
-// rows of fws words; FARMS_FIT_MODE 4), one lane per event: the normal matrix,
-// the PartialPivLU determinant, the adjugate, the ordered (A2 * At) * Y sums
-// and the inlier count -- fit_event_fast's arithmetic in its order, so the
-// plane is bitwise that of every other fit variant.  Events of the quad path
-// issue these per event on all four lanes of their quad; here a wave runs 64
-// events' solves side by side.
-template <int FR>
-__device__ __forceinline__ void fit_solve(const Ctx &c, int w, const uint32_t *fw, int fws) {
-    constexpr int side = 2 * FR + 1, np = side * side;
-    const int4 fd = c.fdesc[w];
-    const int e = fd.x, ex = fd.y, ey = fd.z;
-    if (!c.fit_all && (ex < c.fit_lo || ex >= c.fit_hi)) return;  // a halo event: its owner fits it
-    const uint32_t te = (uint32_t)fd.w;
-    const uint64_t meta = (uint64_t)fw[0] | ((uint64_t)fw[fws] << 32);
-    if (!(meta & kWinFound)) { fit_plane(c, e, 0.0, 0.0, false); return; }
-    const uint64_t vis = meta & ((1ull << np) - 1);
-    const int bw = (int)((meta >> kWinShift) & 15);
-    const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
-    auto cell = [&](int k, int64_t &X, int64_t &Y) {  // k in the reference order: cx-major
-        const int cx = bi + k / side - FR, cy = bj + k % side - FR;
-        const bool vk = (vis >> k) & 1;
-        X = vk ? cx : 0; Y = vk ? cy : 0;
-    };
-    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
-#pragma unroll
-    for (int k = 0; k < np; ++k) {
-        int64_t X, Y;
-        cell(k, X, Y);
-        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
-    }
-    const double a[9] = {(double)sxx, (double)sxy, (double)sx, (double)sxy, (double)syy,
-                         (double)sy,  (double)sx,  (double)sy, (double)np};
-    double DET = det3_partialpivlu(a);
-    if (DET < 1) { fit_plane(c, e, 0.0, 0.0, false); return; }  // 0 inliers
-    DET = 1.0 / DET;  // vFlow.cpp:1327-1336, A2 column-major
-    const double d0 = DET * (a[8] * a[4] - a[7] * a[5]);
-    const double d1 = DET * (a[7] * a[2] - a[8] * a[1]);
-    const double d3 = DET * (a[6] * a[5] - a[8] * a[3]);
-    const double d4 = DET * (a[8] * a[0] - a[6] * a[2]);
-    const double d6 = DET * (a[7] * a[3] - a[6] * a[4]);  // (d2, d5, d8: the intercept row, never used)
-    const double d7 = DET * (a[6] * a[1] - a[7] * a[0]);
-    constexpr bool gemm = (3 + 3 + np) >= 20, gemv = (np + 3 + 1) >= 20;
-    const double cz = (double)te * kTsToSec;
-    double r0 = 0.0, r1 = 0.0;
-#pragma unroll 1
-    for (int k = 0; k < np; ++k) {
-        int64_t Xi, Yi;
-        cell(k, Xi, Yi);
-        const uint32_t T = fw[(2 + k) * fws];
-        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-        double m0, m1;
-        if (gemm) {
-            m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
-            m1 = (((0.0 + d1 * X) + d4 * Y) + d7 * 1.0) + 0.0;
-        } else {
-            m0 = (d0 * X + d3 * Y) + d6 * 1.0;
-            m1 = (d1 * X + d4 * Y) + d7 * 1.0;
-        }
-        if (!gemv && k == 0) { r0 = m0 * yt; r1 = m1 * yt; }
-        else { r0 = r0 + m0 * yt; r1 = r1 + m1 * yt; }
-    }
-    if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
-    const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
-    const double ccx = (double)ex, ccy = (double)ey;
-    int inliers = 0;
-#pragma unroll 1
-    for (int k = 0; k < np; ++k) {
-        int64_t Xi, Yi;
-        cell(k, Xi, Yi);
-        const uint32_t T = fw[(2 + k) * fws];
-        const double Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
-        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
-        const double actualdt = yt - cz;
-        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
-    }
-    fit_plane(c, e, r0, r1, inliers >= c.min_inl);  // vFlow.cpp:934-942
-}
-
-// The solve of fit-chunk positions [s0, s1) on its own (the last chunk of a
-// call in FARMS_FIT_MODE 4).
-template <int FR>
-__global__ __launch_bounds__(64) void k_fit_solve(Ctx c, int s0, int s1, const uint32_t *fw, int fws) {
-    const int w = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (w < s1) fit_solve<FR>(c, w, fw + (w - s0), fws);
-}
-
-// Four lanes per event of chunk [c0, c1) in tile order, the wave's SAE box in
-// LDS (see fit_event_box); lane 0 of the quad stores.  SPLIT (FARMS_FIT_MODE
-// 4): the quads end at the winning window, stored in the chunk's window
-// records (c.fwin, rows of c1 - c0 ... fws words), and the launch also solves
-// the previous chunk's windows (pr.s0 .. pr.s1).
-template <int FR, bool SPLIT>
-__global__ __launch_bounds__(64) void k_fit_box(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
-    const int G = (int)gridDim.x - pr.blocks - pr.sblocks;  // the fit's blocks
-    if ((int)blockIdx.x >= G) {
-        const int b = (int)blockIdx.x - G;
-        if (b < pr.sblocks) {
-            const int w = pr.s0 + b * (int)blockDim.x + (int)threadIdx.x;
-            if (w < pr.s1) fit_solve<FR>(c, w, pr.fw + (w - pr.s0), pr.fws);
-            return;
-        }
-        fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
-                        (b - pr.sblocks) * (int)blockDim.x + (int)threadIdx.x);
-        return;
-    }
-    constexpr int CAP = FitBox<FR>::BOX;
-    __shared__ uint4 s_box[FitBox<FR>::CAP];
-    const int lane = (int)threadIdx.x;
-    const int fb = xcd_block_grouped((int)blockIdx.x, G);
-    const int w = c0 + ((fb * 64 + lane) >> 2);
-    const int j = lane & 3;
-    int4 fd = make_int4(-1, 0, 0, 0);
-    if (w < c1) fd = c.fdesc[w];  // {event, x, y, t}: one 16-B load (k_fit_desc)
-    // halo columns: flows come from their owner (farms_import_flows)
-    const bool active = w < c1 && (c.fit_all || (fd.y >= c.fit_lo && fd.y < c.fit_hi));
-    // ---- the box: bounding box of the union windows of the longest prefix of
-    // the wave's (active) quads that fits CAP cells; wave-uniform scalars
-    const uint64_t act = __ballot(active);
-    int bx0 = INT_MAX, bx1 = INT_MIN, by0 = INT_MAX, by1 = INT_MIN, nin = 0;
-    for (int q = 0; q < 16; ++q) {
-        if (!((act >> (4 * q)) & 1)) continue;
-        const int qx = __builtin_amdgcn_readlane(fd.y, 4 * q), qy = __builtin_amdgcn_readlane(fd.z, 4 * q);
-        const int nx0 = min(bx0, qx), nx1 = max(bx1, qx), ny0 = min(by0, qy), ny1 = max(by1, qy);
-        if ((nx1 - nx0 + 1 + 4 * FR) * (ny1 - ny0 + 1 + 4 * FR) > CAP) break;
-        bx0 = nx0; bx1 = nx1; by0 = ny0; by1 = ny1;
-        nin = q + 1;
-    }
-    const int BX0 = bx0 - 2 * FR, BY0 = by0 - 2 * FR;
-    const int BH = nin ? by1 - by0 + 1 + 4 * FR : 1;
-    const int area = nin ? (bx1 - bx0 + 1 + 4 * FR) * BH : 0;
-    {
-        const float inv = 1.0f / (float)BH;
-        for (int idx = lane; idx < area; idx += 64) {
-            int col = (int)((float)idx * inv);  // idx / BH, corrected below (idx < 2^24)
-            if (col * BH > idx) --col;
-            else if ((col + 1) * BH <= idx) ++col;
-            const int u = BX0 + col, v = BY0 + (idx - col * BH);
-            const bool ok = u >= 0 && u < c.W && u >= c.X0 && u < c.XR1 && v >= 0 && v < c.H;
-            const uint4 hd = sae_head(c, ok ? (uint32_t)((u - c.X0) * c.H + v) : 0u);
-            s_box[idx] = ok ? hd : make_uint4(0, 0, 0, 0);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (!active) return;  // whole quads
-    double vx, vy;
-    bool acc;
-    if constexpr (SPLIT) {
-        uint32_t *fw = c.fwin + (w - c0);
-        uint64_t meta;
-        fit_event_box<FR, true>(c, fd, seq, j, (lane >> 2) < nin, BX0, BY0, BH, s_box, nullptr, vx, vy, acc, fw,
-                                c.fws, &meta);
-        if (j == 0) { fw[0] = (uint32_t)meta; fw[c.fws] = (uint32_t)(meta >> 32); }
-    } else {
-        fit_event_box<FR>(c, fd, seq, j, (lane >> 2) < nin, BX0, BY0, BH, s_box,
-                          reinterpret_cast<uint32_t *>(s_box + CAP) + (lane >> 2), vx, vy, acc);
-        if (j == 0) fit_plane(c, fd.x, vx, vy, acc);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Wave-cooperative fit of one event (any fRad, every lookup complete): the
 // lanes resolve the stamps of the union of the 9 candidate windows into LDS
 // (these lookups are the latency: pixels with many in-chunk events need a run
@@ -2466,19 +2074,12 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
 //   3K + kk fold 1.0 per member: the contributor count of scale kk, exact.
 // LDS (private to the wave): s_val / s_k0 the values {L, L cos, L sin, 1} and k0 of one step's
 // 64 staged entries (contributors first, in rank order).
-// G (group pooling, k_pool<K, W7, true>): the flattened positions are those of
-// the union window of the event's (chunk, tile) group, whose candidate headers
-// the wave staged in LDS (g_hdr, and g_kr = row << 25 | candidate index); a
-// position takes part iff its cell lies in the event's own window gw = {i_lo,
-// i_hi, j_lo, j_hi}.  The union's row slices contain the event's row slices
-// as contiguous sub-ranges (same clipping), so the positions that take part,
-// in order, are exactly the event's own flattened sequence.
-template <int K, bool G>
+template <int K>
+__device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, double acc, int scanned, int ncon_total);
+template <int K>
 __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
                                          int row_i0, int total, int ev0, const uint64_t *s_start,
-                                         const uint32_t *s_row, double *s_val, uint8_t *s_k0,
-                                         const uint4 *g_hdr = nullptr, const uint32_t *g_kr = nullptr,
-                                         int4 gw = int4{}) {
+                                         const uint32_t *s_row, double *s_val, uint8_t *s_k0) {
     static_assert(4 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
@@ -2516,31 +2117,16 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             k[h] = f0 + 64 * h + lane + (int)(rs & 0x1FFFFFFu) - kRowBias;
         }
     };
-    // G: the staged header, row and candidate index of position f
-    auto staged = [&](int f, int &row, int &k, CandHdr &hd) {
-        const uint4 u = g_hdr[f];
-        const uint32_t kr = g_kr[f];
-        hd = CandHdr{u.x, (int)u.y, u.z, u.w};
-        row = (int)(kr >> 25);
-        k = (int)(kr & 0x1FFFFFFu);
-    };
     int rc[NH], kc[NH];
     CandHdr hc[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) { rc[h] = 0; kc[h] = 0; hc[h] = CandHdr{}; }
     if (total > 0) {
-        if constexpr (G) {
+        locate(0, rc, kc);
 #pragma unroll
-            for (int h = 0; h < NH; ++h)
-                if (64 * h + lane < total) staged(64 * h + lane, rc[h], kc[h], hc[h]);
-        } else {
-            locate(0, rc, kc);
-#pragma unroll
-            for (int h = 0; h < NH; ++h)
-                if (64 * h + lane < total) hc[h] = chdr[kc[h]];
-        }
+        for (int h = 0; h < NH; ++h)
+            if (64 * h + lane < total) hc[h] = chdr[kc[h]];
     }
-    int nin = 0;  // G: positions in the event's window (the candidates it scans)
     // the previous step's contributors: ballots, values, smallest scales
     uint64_t pbal[NH];
     double pv[NH][3];
@@ -2557,14 +2143,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             con[h] = false;
             k0[h] = K;
             vp[h] = vdummy;
-            bool inw = have && f0 + 64 * h + lane < total;
-            if constexpr (G) {
-                const int i = row_i0 + rc[h];
-                const int j = (int)(hc[h].lin & kCandLinMask) + OFF - i * H;
-                inw = inw && i >= gw.x && i <= gw.y && j >= gw.z && j <= gw.w;
-                nin += (int)__popcll(__ballot(inw));
-            }
-            if (inw) {
+            if (have && f0 + 64 * h + lane < total) {
                 const CandHdr &hd = hc[h];
                 uint32_t tq;
                 bool ok;
@@ -2601,16 +2180,10 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 #pragma unroll
         for (int h = 0; h < NH; ++h) { rn[h] = 0; kn[h] = 0; hn[h] = CandHdr{}; }
         if (f0 + 64 * NH < total) {
-            if constexpr (G) {
+            locate(f0 + 64 * NH, rn, kn);
 #pragma unroll
-                for (int h = 0; h < NH; ++h)
-                    if (f0 + 64 * (NH + h) + lane < total) staged(f0 + 64 * (NH + h) + lane, rn[h], kn[h], hn[h]);
-            } else {
-                locate(f0 + 64 * NH, rn, kn);
-#pragma unroll
-                for (int h = 0; h < NH; ++h)
-                    if (f0 + 64 * (NH + h) + lane < total) hn[h] = chdr[kn[h]];
-            }
+            for (int h = 0; h < NH; ++h)
+                if (f0 + 64 * (NH + h) + lane < total) hn[h] = chdr[kn[h]];
         }
         // ---- stage and fold the previous step's contributors
         uint64_t pany = 0;
@@ -2658,8 +2231,16 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             hc[h] = hn[h]; rc[h] = rn[h]; kc[h] = kn[h];
         }
     }
-    // first strict max of the mean length over scales (vFlow.cpp:1023-1059):
-    // the winner is the lowest k whose mean equals the maximum, if it is > 0
+    pool_finish<K>(c, e, lane, acc, total, ncon_total);
+}
+
+// Every per-scale sum of event e folded (lane g * K + kk holds quantity g of
+// scale kk): the first strict max of the mean length over scales
+// (vFlow.cpp:1023-1059) -- the winner is the lowest k whose mean equals the
+// maximum, if it is > 0 -- and the event's global flow vector.
+template <int K>
+__device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, double acc, int scanned, int ncon_total) {
+    const int J = c.J;
     const double cnt_kk = __shfl(acc, 3 * K + (lane < K ? lane : 0), 64);  // contributors of scale lane
     const bool is_len = lane < K;
     const double mean = is_len && cnt_kk > 0 ? acc / cnt_kk : 0.0;
@@ -2680,7 +2261,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         c.r_true[e] = gx;  // (RTrue, ThetaTrue) by k_true_polar, 64 events per wave
         c.th_true[e] = gy;
         c.scale[e] = sc;
-        if (c.dbg_tc) c.dbg_tc[e] = make_int2(G ? nin : total, ncon_total);
+        if (c.dbg_tc) c.dbg_tc[e] = make_int2(scanned, ncon_total);
     }
 }
 
@@ -2693,116 +2274,7 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
-    pool_one<K, false>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0);
-}
-
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) v = min(v, __shfl_xor(v, s, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) v = max(v, __shfl_xor(v, s, 64));
-    return v;
-}
-
-// Group pooling: the wave of a (chunk, tile) group's first work-order position
-// pools every valid owned event of the group.  Their windows overlap almost
-// entirely (one 8x8 tile of centres), so the wave builds the row table of the
-// union of their windows once and stages the union's candidate headers in LDS
-// once; each event then resolves its candidates from LDS (pool_one<K, true>)
-// instead of issuing its own descriptor, row-word and header round trips to
-// L2.  Its values are still loaded per contributor, and its fold is the
-// per-event fold in the reference order, so the records are bitwise those of
-// pool_event.  A group with one valid event, a union of more than 128 rows or
-// more than pool_capg candidates pools its events one by one.
-template <int K>
-__device__ __forceinline__ void pool_group(const Ctx &c, int w, int buf, int lane, uint64_t *s_start, uint32_t *s_row,
-                                           double *s_val, uint8_t *s_k0, uint4 *s_hdr, uint32_t *s_kr) {
-    const int W = c.W, M = c.M;
-    const uint32_t key = c.gkey[w];
-    // pass 1: the group's extent [w, wend) (contiguous positions with its key,
-    // in batches of 64), its valid events' count and bounding box
-    int nv = 0, xmin = INT_MAX, xmax = -1, ymin = INT_MAX, ymax = -1, wend = w;
-    for (int b0 = w;; b0 += 64) {
-        const int pos = b0 + lane;
-        const bool inr = pos < c.n;
-        const int pc = inr ? pos : w;
-        const uint32_t kq = c.gkey[pc];  // unconditional loads from a clamped index
-        const int4 q = c.qe[pc];
-        const bool ing = inr && kq == key;
-        const uint64_t gm = __ballot(ing);  // a prefix of the batch: keys are sorted
-        const bool v = ing && q.x >= 0;
-        nv += (int)__popcll(__ballot(v));
-        const int qx = q.y & ~kLeadBit;
-        xmin = min(xmin, wave_min_i(v ? qx : INT_MAX));
-        xmax = max(xmax, wave_max_i(v ? qx : -1));
-        ymin = min(ymin, wave_min_i(v ? q.z : INT_MAX));
-        ymax = max(ymax, wave_max_i(v ? q.z : -1));
-        if (gm != ~0ull) { wend = b0 + (int)__popcll(gm); break; }
-    }
-    if (nv == 0) return;
-    const int ui_lo = max(xmin - M, 0), ui_hi = min(xmax + M, W - 1);
-    const int uj_lo = max(ymin - M, 0), uj_hi = min(ymax + M, W - 1);
-    bool grp = nv >= 2 && ui_hi - ui_lo + 1 <= 128 && c.pool_capg > 0;
-    int total = 0;
-    if (grp) {
-        total = pool_rows(c, buf, lane, ui_lo, ui_hi - ui_lo + 1, uj_lo, uj_hi, s_start, s_row);
-        grp = total <= c.pool_capg;
-    }
-    if (grp) {
-        // stage the union's headers: four steps' loads in flight at a time
-        const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
-        int mbase = 0;
-        for (int f0 = 0; f0 < total; f0 += 256) {
-            uint4 hv[4];
-            uint32_t kr[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int f = f0 + 64 * s;
-                const uint64_t mk = f < total ? s_start[f >> 6] : 0ull;
-                const int m = mbase + (int)__popcll(mk & ((2ull << lane) - 1)) - 1;
-                mbase += (int)__popcll(mk);
-                const uint32_t rs = s_row[m < 0 ? 0 : m];
-                const int k = f + lane + (int)(rs & 0x1FFFFFFu) - kRowBias;
-                const bool ok = f + lane < total;
-                kr[s] = (rs & 0xFE000000u) | (uint32_t)(ok ? k : 0);
-                hv[s] = reinterpret_cast<const uint4 *>(chdr)[ok ? k : 0];
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int f = f0 + 64 * s + lane;
-                if (f < total) { s_hdr[f] = hv[s]; s_kr[f] = kr[s]; }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    // pass 2: the group's valid events, in work order
-    for (int b0 = w; b0 < wend; b0 += 64) {
-        const int pos = b0 + lane;
-        const int4 q = c.qe[pos < wend ? pos : w];
-        uint64_t vm = __ballot(pos < wend && q.x >= 0);
-        while (vm) {
-            const int l = (int)__builtin_ctzll(vm);
-            vm &= vm - 1;
-            const int e = __builtin_amdgcn_readlane(q.x, l);
-            const int ex = __builtin_amdgcn_readlane(q.y, l) & ~kLeadBit;
-            const int ey = __builtin_amdgcn_readlane(q.z, l);
-            const uint32_t teu = (uint32_t)__builtin_amdgcn_readlane(q.w, l);
-            if (grp) {
-                const int4 gw = make_int4(max(ex - M, 0), min(ex + M, W - 1), max(ey - M, 0), min(ey + M, W - 1));
-                pool_one<K, true>(c, e, ex, ey, teu, buf, lane, ui_lo, total, 0, s_start, s_row, s_val, s_k0, s_hdr,
-                                  s_kr, gw);
-            } else {
-                pool_event<K>(c, e, ex, ey, teu, buf, lane, 0, s_start, s_row, s_val, s_k0);
-            }
-            // the next event's staging reuses s_val / s_k0 (and, one by one, the row table)
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
+    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0);
 }
 
 // One wavefront (= one workgroup, so that a finished event frees its slot at
@@ -2811,7 +2283,7 @@ __device__ __forceinline__ void pool_group(const Ctx &c, int w, int buf, int lan
 // once.
 #define FARMS_POOL_FLOOR_7 "v71"  // k_pool occupancy cap of 7 waves per SIMD (see k_pool)
 #define FARMS_POOL_FLOOR_6 "v79"  // k_pool occupancy cap of 6 waves per SIMD
-template <int K, bool W7, bool G>
+template <int K, bool W7>
 __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     // LDS per wave, sized for maxWindow M at launch: segment-start bitmap over
     // the flattened window, <= 2 row segments per window row, the values and
@@ -2837,18 +2309,11 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     if (w >= c1) return;
     // the event and its fields in one 16-B load (k_pool_desc)
     const int4 d = c.qe[w];
+    if (d.x < 0) return;  // invalid flow, or a halo event (pooled by its owner)
+    const int e = d.x, ex = d.y, ey = d.z;
+    const uint32_t teu = (uint32_t)d.w;
     const int buf = (c.ring0 + w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    if constexpr (G) {
-        if (!(d.y & kLeadBit)) return;  // pooled by its group's wave
-        uint4 *s_hdr = reinterpret_cast<uint4 *>(s_start + ((nbw + nrs + kPoolValWords + 1) & ~1));  // 16-B aligned
-        uint32_t *s_kr = reinterpret_cast<uint32_t *>(s_hdr + c.pool_capg);
-        pool_group<K>(c, w, buf, lane, s_start, s_row, s_val, s_k0, s_hdr, s_kr);
-    } else {
-        if (d.x < 0) return;  // invalid flow, or a halo event (pooled by its owner)
-        const int e = d.x, ex = d.y & ~kLeadBit, ey = d.z;
-        const uint32_t teu = (uint32_t)d.w;
-        pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
-    }
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -3031,7 +2496,6 @@ struct farms_handle {
     SaeTail *sae_tail = nullptr;  // two of WH tails
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    uint32_t *fwin = nullptr;  // FARMS_FIT_MODE 4: window records of two fit chunks (allocated on first use)
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1), indexed by
     // the chunk's number since the last reset (calls continue the ring)
     int pool_batch = kDefaultPoolBatch, NB = 2 * kDefaultPoolBatch + 1;
@@ -3265,14 +2729,8 @@ int reset_surfaces(farms_handle *h) {
 
 template <int K, bool W7>
 void launch_pool(const Ctx &c, int c0, int c1, hipStream_t s) {
-    if (c.pool_capg > 0) {  // group pooling: + the staged headers (16 B) and their row / index words (4 B)
-        const size_t words = (size_t)((c.pool_bw + c.pool_rs + kPoolValWords + 1) & ~1);
-        const size_t lds = sizeof(uint64_t) * words + 20 * (size_t)c.pool_capg;
-        hipLaunchKernelGGL((k_pool<K, W7, true>), dim3(c1 - c0), dim3(64), lds, s, c, c0, c1);
-        return;
-    }
     const size_t lds = sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
-    hipLaunchKernelGGL((k_pool<K, W7, false>), dim3(c1 - c0), dim3(64), lds, s, c, c0, c1);
+    hipLaunchKernelGGL((k_pool<K, W7>), dim3(c1 - c0), dim3(64), lds, s, c, c0, c1);
 }
 
 typedef void (*pool_launcher)(const Ctx &, int, int, hipStream_t);
@@ -3301,35 +2759,19 @@ pool_launcher pool_for(int K, int fr) {
 }
 // Tuning knobs of the fit (A/B aids; every choice gives the same bits):
 // FARMS_FIT_QUAD=0: one thread per event; FARMS_FIT_MODE 0 = re-gather the
-// winning window, 1 = union tile with columns per lane, 2 = union tile with
-// rows per lane, 3 = the wave's SAE box in LDS (default), 4 = the box scan
-// ending at the winning window, then one lane per event for the solve
-// (fit_solve, riding on the next chunk's fit launch).
+// winning window, 1 = union tile with columns per lane (default), 2 = union
+// tile with rows per lane.  (Round 4 also measured a wave-wide SAE box in LDS
+// and a split of the fit into that box scan plus one lane per event for the
+// LU and the ordered sums: C3 / C4 106.7 / 102.4 and 105.4 / 103.4 ms per
+// step against 88.9 / 86.9 for mode 1; removed.  DESIGN.md §8.)
 bool fit_quad_env() {
     const char *fq = getenv("FARMS_FIT_QUAD");
     return !(fq && fq[0] == '0');
 }
 int fit_mode_env() {
     const char *fu = getenv("FARMS_FIT_MODE");
-    const int m = fu ? atoi(fu) : 3;
-    return m >= 0 && m <= 4 ? m : 3;
-}
-// Group pooling (FARMS_POOL_GROUP=0: one wave per event) for windows whose
-// union over a work-order tile fits the 128-row table.
-bool pool_group_on(const farms_handle *h) {
-    const char *pg = getenv("FARMS_POOL_GROUP");
-    return !(pg && pg[0] == '0') && 2 * h->M + (1 << h->tile_shift) <= 128;
-}
-
-// FARMS_FIT_MODE 4: the solve of fit-chunk positions [s0, s1) on its own.
-void launch_solve(const Ctx &c, int fr, int s0, int s1, const uint32_t *fw, int fws, hipStream_t s) {
-    const dim3 g(ceil_div(s1 - s0, 64)), b(64);
-    switch (fr) {
-    case 1: hipLaunchKernelGGL(k_fit_solve<1>, g, b, 0, s, c, s0, s1, fw, fws); break;
-    case 2: hipLaunchKernelGGL(k_fit_solve<2>, g, b, 0, s, c, s0, s1, fw, fws); break;
-    case 3: hipLaunchKernelGGL(k_fit_solve<3>, g, b, 0, s, c, s0, s1, fw, fws); break;
-    default: break;
-    }
+    const int m = fu ? atoi(fu) : 1;
+    return m >= 0 && m <= 2 ? m : 1;
 }
 
 // Fit of chunk [c0, c1); pr.blocks > 0: with the next chunk's prep riding on
@@ -3337,11 +2779,9 @@ void launch_solve(const Ctx &c, int fr, int s0, int s1, const uint32_t *fw, int 
 bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t s, bool quad, int mode,
                 FitPrep pr) {
     if (quad) {
-        const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks + pr.sblocks), b(64);
+        const dim3 g(ceil_div(c1 - c0, kFitQS) + pr.blocks), b(64);
 #define FARMS_FIT_CASE(FR_)                                                                            \
-    if (mode == 4) hipLaunchKernelGGL((k_fit_box<FR_, true>), g, b, 0, s, c, c0, c1, seq, pr);        \
-    else if (mode == 3) hipLaunchKernelGGL((k_fit_box<FR_, false>), g, b, 0, s, c, c0, c1, seq, pr);  \
-    else if (mode == 2) hipLaunchKernelGGL((k_fit_quad<FR_, 2>), g, b, 0, s, c, c0, c1, seq, pr);     \
+    if (mode == 2) hipLaunchKernelGGL((k_fit_quad<FR_, 2>), g, b, 0, s, c, c0, c1, seq, pr);          \
     else if (mode == 1) hipLaunchKernelGGL((k_fit_quad<FR_, 1>), g, b, 0, s, c, c0, c1, seq, pr);     \
     else hipLaunchKernelGGL((k_fit_quad<FR_, 0>), g, b, 0, s, c, c0, c1, seq, pr);                    \
     return true;
@@ -3409,14 +2849,7 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.ring0 = (int)(h->chunk_base % h->NB);
-    // group pooling (FARMS_POOL_GROUP=0: one wave per event; A/B aid), for
-    // windows whose union over a work-order tile fits the 128-row table
-    const int tile = 1 << h->tile_shift;
-    const bool group = pool_group_on(h);
-    c.gkey = w.wkey_sorted;
-    c.pool_capg = group ? kPoolGroupCap : 0;
-    // pooling window rows and columns (group: of the union of a tile's windows)
-    const int span = 2 * h->M + (group ? tile : 1);
+    const int span = 2 * h->M + 1;  // pooling window rows and columns
     c.pool_bw = (span * span + 63) / 64 + 1;  // flattened window positions (+1: a two-half step reads a word ahead)
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
     c.r_true = dout->r_true; c.th_true = dout->theta_true; c.vx = dout->vx; c.vy = dout->vy;
@@ -3561,17 +2994,6 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const bool fit_quad = fit_quad_env();
     const int fit_mode = fit_mode_env();
-    const bool split = fast_fit && fit_quad && fit_mode == 4;
-    if (split && !h->fwin) {  // two chunks' window records (the scanned chunk and the one being solved)
-        const int np = (2 * h->fr + 1) * (2 * h->fr + 1);
-        int rc = dalloc(&h->fwin, 2 * (size_t)(2 + np) * (size_t)h->fit_chunk);
-        if (rc) return rc;
-    }
-    auto fwin_of = [&](int f) { return h->fwin + (size_t)(f & 1) * (size_t)(2 + (2 * h->fr + 1) * (2 * h->fr + 1)) *
-                                                     (size_t)h->fit_chunk; };
-    // fit chunk f's planes are final once ev_fit(f) is recorded: after its own
-    // launch, or (split) after the next chunk's launch, which solves it
-    auto fit_recorded = [&](int f, int enq) { return split ? (f < enq - 1 || enq == n_fit_chunks) : f < enq; };
     int fit_launches = 0;
     auto fit_chunk_end = [&](int f) { return (int)std::min<int64_t>((int64_t)(f + 1) * h->fit_chunk, n); };
     // The SAE is double-buffered by chunk parity (buffer f % 2 serves chunk f),
@@ -3599,17 +3021,6 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         cf.cells = cells_of(f);
         FitPrep next{};
         if (f + 1 < n_fit_chunks) next = prep_of(f + 1);
-        if (split) {  // this chunk's windows; the previous chunk's solve rides on the launch
-            cf.fwin = fwin_of(f);
-            cf.fws = h->fit_chunk;
-            if (f > 0) {
-                next.s0 = fit_start(f - 1);
-                next.s1 = fit_chunk_end(f - 1);
-                next.sblocks = ceil_div(next.s1 - next.s0, 64);
-                next.fw = fwin_of(f - 1);
-                next.fws = h->fit_chunk;
-            }
-        }
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (prof && h->fit_events) { int rc = mark(h, s, &k0); if (rc) return rc; }
         bool merged = false;
@@ -3620,20 +3031,12 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
                                c1 - c0);
         }
         if (!merged && next.blocks > 0) launch_prep(next);
-        if (split && f == n_fit_chunks - 1) {  // the last chunk's solve on its own
-            launch_solve(cf, h->fr, c0, c1, fwin_of(f), h->fit_chunk, s);
-            ++fit_launches;
-        }
         if (k0) {
             int rc = mark(h, s, &k1);
             if (rc) return rc;
             h->brk.push_back({k0, k1, kBrFitKernel});
         }
-        if (!split) HIPCHK(hipEventRecord(ev_fit(f), s));
-        else {
-            if (f > 0) HIPCHK(hipEventRecord(ev_fit(f - 1), s));
-            if (f == n_fit_chunks - 1) HIPCHK(hipEventRecord(ev_fit(f), s));
-        }
+        HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
             FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
@@ -3692,10 +3095,6 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         {  // the chain reads the local flows of every event of the super-chunk
             const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
             const int fl = std::min(f, n_fit_chunks - 1);
-            while (!fit_recorded(fl, fit_enqueued)) {  // (split: the launch that solves it)
-                int rc = enqueue_fit(fit_enqueued++);
-                if (rc) return rc;
-            }
             if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
         }
         if (phase != 2) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
@@ -3929,7 +3328,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     if (h->s_chain) (void)hipStreamSynchronize(h->s_chain);
     if (h->s_pool) (void)hipStreamSynchronize(h->s_pool);
     if (h->s_copy) (void)hipStreamSynchronize(h->s_copy);
-    dfree(h->sae_head); dfree(h->sae_tail); dfree(h->ftime); dfree(h->fsnap); dfree(h->fwin);
+    dfree(h->sae_head); dfree(h->sae_tail); dfree(h->ftime); dfree(h->fsnap);
     for (Work &w : h->ws) {
         free_workspace(w);
         dfree(w.pcur); dfree(w.pend);
@@ -3997,16 +3396,13 @@ extern "C" int farms_kernel_info(const farms_handle *h, char *buf, int32_t len) 
     const bool fast = h->fr >= 1 && h->fr <= 3, quad = fit_quad_env();
     const int mode = fit_mode_env();
     const std::string fr = std::to_string(h->fr);
-    std::string fit, solve;
+    std::string fit;
     if (!fast) fit = "k_fit_wave";
     else if (!quad) fit = "k_fit<" + fr + ">";
-    else if (mode >= 3) fit = "k_fit_box<" + fr + ">";
     else fit = "k_fit_quad<" + fr + ">";
-    if (fast && quad && mode == 4) solve = "k_fit_box<" + fr + ">+k_fit_solve<" + fr + ">";
-    const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(quad ? mode : -1) +
-                           ", \"fit_solve\": \"" + solve + "\", \"pool\": \"k_pool<" + std::to_string(h->K) +
-                           ">\", \"pool_group\": " + (pool_group_on(h) ? "1" : "0") +
-                           ", \"pool_cap\": " + (pool_w7(h->fr) ? "7" : "6") + "}";
+    const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(fast && quad ? mode : -1) +
+                           ", \"pool\": \"k_pool<" + std::to_string(h->K) + ">\", \"pool_cap\": " +
+                           (pool_w7(h->fr) ? "7" : "6") + "}";
     std::snprintf(buf, (size_t)len, "%s", js.c_str());
     return FARMS_OK;
 }

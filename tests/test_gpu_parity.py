@@ -148,20 +148,16 @@ def test_chunking_is_bitwise_invariant():
 
 
 def test_pool_variants_are_bitwise_invariant(monkeypatch):
-    """k_pool is built four ways (7- and 6-wave VGPR floors, pool_for picks by
-    filter size; group pooling -- one wave per (chunk, tile) group with the
-    union window's headers in LDS -- or one wave per event,
-    FARMS_POOL_GROUP=0): every build gives the same bits."""
+    """k_pool is built twice (7- and 6-wave VGPR floors, pool_for picks by
+    filter size): both builds give the same bits."""
     ev = farms.synth_config(3, 120_000)
     x, y, t, p = ev.relative()
     outs = []
-    for cap, grp in (("7", "1"), ("6", "1"), ("7", "0"), ("6", "0")):
+    for cap in ("7", "6"):
         monkeypatch.setenv("FARMS_POOL_CAP", cap)
-        monkeypatch.setenv("FARMS_POOL_GROUP", grp)
         with farms.FlowManager(720, 1280, 5, 5) as fm:
             outs.append(fm.process(x, y, t, p))
-    for o in outs[1:]:
-        assert bitwise_equal(outs[0], o)
+    assert bitwise_equal(outs[0], outs[1])
 
 
 def test_streaming_split_equals_one_call():
@@ -261,14 +257,12 @@ def test_out_of_sensor_event_is_rejected():
 @pytest.mark.parametrize("fs", [3, 5, 7])
 def test_fit_variants_are_bitwise_identical(fs, monkeypatch):
     """The quad-lane fits (FARMS_FIT_MODE 0: re-gathered winning window, 1:
-    union tile by columns, 2: union tile by rows, 3: the wave's SAE box in LDS,
-    4: the box scan ending at the winning window, then one lane per event)
-    and the one-thread fit evaluate the same arithmetic in the same order:
-    bitwise-equal records."""
+    union tile by columns, 2: union tile by rows) and the one-thread fit
+    evaluate the same arithmetic in the same order: bitwise-equal records."""
     ev = farms.synth_config(3, 150_000)
     x, y, t, p = ev.relative()
     outs = []
-    for quad, mode in [("1", "3"), ("1", "0"), ("1", "1"), ("1", "2"), ("1", "4"), ("0", "3")]:
+    for quad, mode in [("1", "1"), ("1", "0"), ("1", "2"), ("0", "1")]:
         monkeypatch.setenv("FARMS_FIT_QUAD", quad)
         monkeypatch.setenv("FARMS_FIT_MODE", mode)
         with farms.FlowManager(720, 1280, fs, 5) as fm:

@@ -78,8 +78,11 @@ def parse():
                     help="N=1: steps of the host-array path (farms_process: H2D + kernels + D2H) timed after "
                          "the device-resident ones (0 = skip)")
     ap.add_argument("--prof", choices=("timing", "pool"), default="timing",
-                    help="HIP-event brackets in the timed steps: around every fit and pooling launch (timing), or "
-                         "the pooling launches only (pool)")
+                    help="HIP-event brackets in the profiled steps: around every fit and pooling launch (timing), "
+                         "or the pooling launches only (pool)")
+    ap.add_argument("--prof-steps", type=int, default=2,
+                    help="steps after the timed ones with HIP-event brackets (the kernel timings of the roofline); "
+                         "the timed steps run without them")
     ap.add_argument("--plan-only", action="store_true",
                     help="launch, rendezvous, per-rank stream shares and partition only; no GPU, no timing "
                          "(CPU test of the multi-rank plumbing; value is null)")
@@ -387,26 +390,34 @@ def main():
     st = multirank.Stepper(fm, sh, dist, device, xdev)
     torch.cuda.synchronize()
 
-    # HIP events around the phases and every fit and pooling launch, on the
-    # streams that run them (farms_stats sums them over a step's calls)
-    fm.set_profiling(farms.PROF_TIMING if args.prof == "timing" else farms.PROF_POOL)
+    # the timed steps run uninstrumented (HIP-event brackets around every fit
+    # launch cost 4-6 ms per step); the kernel timings come from prof_steps
+    # more steps with HIP events around the phases and every fit and pooling
+    # launch, on the streams that run them (farms_stats sums them over a
+    # step's calls)
+    fm.set_profiling(0)
     if dist:
         dist.barrier()  # communicators up on every rank before the first exchange
     for _ in range(args.warmup):
         st.step()
-    stats = []
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st.step()
-        stats.append(fm.stats())
     torch.cuda.synchronize()
     elapsed_rank = time.perf_counter() - t0  # this rank's own steps, before waiting for the others
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    fm.set_profiling(farms.PROF_TIMING if args.prof == "timing" else farms.PROF_POOL)
+    stats = []
+    for _ in range(max(args.prof_steps, 1)):
+        st.step()
+        stats.append(fm.stats())
+    if dist:
+        dist.barrier()
     if dist:
         tt = torch.tensor([elapsed], device=xdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -420,7 +431,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = total_events * args.steps / elapsed / 1e6
     mean = {k: sum(s_[k] for s_ in stats) / len(stats) for k in ("ms_fit_kernel", "ms_pool_kernel")}
-    ts = dict(stats[-1], **mean)  # launch counts of a step, kernel times averaged over the timed steps
+    ts = dict(stats[-1], **mean)  # launch counts of a step, kernel times averaged over the profiled steps
     # work counters (U_loc, U_pool, candidates, contributors) from one more, untimed step
     fm.set_profiling(True)
     st.step()
@@ -462,7 +473,7 @@ def main():
                    "ms_pool_sweep": round(ts["ms_pool"], 3), "ms_fit_kernel": round(ts["ms_fit_kernel"], 3),
                    "ms_pool_kernel": round(ts["ms_pool_kernel"], 3),
                    "fit_launches": ts["fit_launches"], "pool_launches": ts["pool_launches"],
-                   "profiling": args.prof,
+                   "profiling": f"{args.prof}, {max(args.prof_steps, 1)} steps after the timed ones",
                    "dense_equiv_bytes_per_event": round(20.0 * cs["pool_cells"] / max(n_owned, 1), 1),
                    "cand_per_valid": round(cs["pool_candidates"] / max(cs["n_valid"], 1), 1),
                    "contrib_per_valid": round(cs["pool_contributors"] / max(cs["n_valid"], 1), 1)},

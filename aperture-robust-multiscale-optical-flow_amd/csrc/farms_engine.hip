@@ -93,22 +93,29 @@ struct __attribute__((aligned(32))) FlowCell {
 // SAE cell (x-major): snapshot of the SAE at chunk start plus the first two
 // events of the current chunk at this pixel, inline, so "stamp as of e" is
 // resolved without pointer chasing unless the pixel fired three or more times
-// in the chunk (a bar's ON/OFF pair is the common case).  Two arrays of 16-B
-// records: the head, read by every window scan (eight cells per 128-B line,
-// so the four lanes of a fit quad reading four consecutive rows touch one
-// line), and the tail, read only when a pixel fired twice in the chunk.
-// head: tag: bit31 = snapshot visited, bits 0..30 = seq of the chunk that last
-//   touched the pixel; e1m: first in-chunk event id, bit31 = more than one
-//   in-chunk event; t1: its stamp; tsnap: the snapshot stamp.
+// in the chunk (a bar's ON/OFF pair is the common case).  Two arrays: the
+// 12-B head, read by every window scan (a column of 13 cells is 156 B, loaded
+// as dwordx3), and the 16-B tail, read only when a pixel fired twice in the
+// chunk.
+// head: tsnap: the snapshot stamp; t1: the first in-chunk event's stamp; w:
+//   kHeadTouched = the pixel fired in the current fit chunk (e1, t1, the tail
+//   are current; the chunk's prep sets it and clears it again when it commits
+//   the pixel's last event to the snapshot, so no chunk sequence number is
+//   kept), kHeadMore = more than one in-chunk event, kHeadVisited = the
+//   snapshot is valid, bits 0..28 = e1, the first in-chunk event's id.
 // tail: e2m: second in-chunk event id, bit31 = more than two (then the pixel's
 //   run [run_lo, run_hi] of positions in P, scanned in PT, resolves later
 //   events); t2: its stamp.
-struct __attribute__((aligned(16))) SaeHead {
-    uint32_t tag;
-    uint32_t e1m;
-    uint32_t t1;
+struct SaeHead {
     uint32_t tsnap;
+    uint32_t t1;
+    uint32_t w;
 };
+constexpr uint32_t kHeadTouched = 0x80000000u, kHeadMore = 0x40000000u, kHeadVisited = 0x20000000u;
+constexpr uint32_t kHeadE1Mask = 0x1FFFFFFFu;
+// events of one device call (their ids fit the head's 29 bits); farms_process
+// cuts longer host calls into sub-batches below it
+constexpr int64_t kMaxCallEvents = (int64_t)kHeadE1Mask;
 struct __attribute__((aligned(16))) SaeTail {
     uint32_t e2m;
     uint32_t t2;
@@ -229,25 +236,28 @@ __device__ __forceinline__ uint32_t run_asof(const Ctx &c, int lo, int hi, int e
     return t;
 }
 
-// SAE stamp of pixel q as of event e (chunk seq): -1 never visited, else t.
-// h is the cell's first 16 B (tag, e1m, t1, tsnap); the second half (second
-// event, run bounds) is loaded only when it decides the answer.
-__device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint4 h, uint32_t q, int e, uint32_t seq) {
-    if ((h.x & kSeqMask) == seq) {
-        const int e1 = (int)(h.y & kSeqMask);
+// SAE stamp of pixel q as of event e: -1 never visited, else t.  h is the
+// cell's head {tsnap, t1, w}; the tail (second event, run bounds) is loaded
+// only when it decides the answer.  (seq: unused, the head's kHeadTouched
+// marks in-chunk state of the current chunk.)
+__device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint3 h, uint32_t q, int e, uint32_t seq) {
+    (void)seq;
+    if (h.z & kHeadTouched) {
+        const int e1 = (int)(h.z & kHeadE1Mask);
         if (e1 <= e) {
-            if (!(h.y >> 31)) return (int64_t)h.z;
+            if (!(h.z & kHeadMore)) return (int64_t)h.y;
             const uint4 g = reinterpret_cast<const uint4 *>(c.cells.tail)[q];  // e2m, t2, run_lo, run_hi
-            if ((int)(g.x & kSeqMask) > e) return (int64_t)h.z;
+            if ((int)(g.x & kSeqMask) > e) return (int64_t)h.y;
             if (!(g.x >> 31)) return (int64_t)g.y;
             return (int64_t)run_asof(c, (int)g.z, (int)g.w, e, g.y);
         }
     }
-    return (h.x >> 31) ? (int64_t)h.w : int64_t(-1);
+    return (h.z & kHeadVisited) ? (int64_t)h.x : int64_t(-1);
 }
 
-__device__ __forceinline__ uint4 sae_head(const Ctx &c, uint32_t q) {
-    return reinterpret_cast<const uint4 *>(c.cells.head)[q];
+__device__ __forceinline__ uint3 sae_head(const Ctx &c, uint32_t q) {
+    const SaeHead hd = c.cells.head[q];  // one dwordx3 load
+    return make_uint3(hd.tsnap, hd.t1, hd.w);
 }
 
 __device__ __forceinline__ int64_t sae_asof(const Ctx &c, uint32_t q, int e, uint32_t seq) {
@@ -377,7 +387,7 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeBuf cells, int 
         const int nx = c.link[ep].z;
         if (nx >= c0 && nx >= c1) {  // last event of chunk f-1 at a pixel chunk f does not touch
             SaeHead *hd = &cells.head[c.pix[ep]];
-            hd->tag |= 0x80000000u;
+            hd->w = kHeadVisited;  // committed: no longer touched (stale state of chunk f-2 cleared)
             hd->tsnap = c.t[ep];
         }
     }
@@ -389,13 +399,10 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeBuf cells, int 
     if (lk.y < c0) {  // first event of the pixel in the chunk
         SaeHead *hd = &cells.head[q];
         SaeTail *tl = &cells.tail[q];
-        if (lk.y >= 0) {
-            hd->tag = seq | 0x80000000u;
-            hd->tsnap = (uint32_t)lk.w;
-        } else {  // no earlier event in this call: keep the snapshot of earlier calls
-            hd->tag = (hd->tag & 0x80000000u) | seq;
-        }
-        hd->e1m = (uint32_t)e | (nx < c1 ? 0x80000000u : 0u);
+        uint32_t vis = kHeadVisited;
+        if (lk.y >= 0) hd->tsnap = (uint32_t)lk.w;
+        else vis = hd->w & kHeadVisited;  // no earlier event in this call: keep the snapshot of earlier calls
+        hd->w = vis | kHeadTouched | (nx < c1 ? kHeadMore : 0u) | (uint32_t)e;
         hd->t1 = c.t[e];
         tl->run_lo = lk.x;
         if (nx < c1) {  // and the second one
@@ -645,7 +652,7 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t s
     // column's stamps give three vertical partial sums, which are added to the
     // windows whose column range contains it.  Every window's score is the
     // same integer sum in any order.
-    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+    auto load_col = [&](int u0, int v0, int len, uint3 *col) {
         const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
         const int cbase = (u0 - c.X0) * H + v0;
 #pragma unroll
@@ -654,11 +661,11 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t s
             // unconditional load from a clamped index, then select: a load under a
             // branch is waited for at the branch's end, serializing the column
             const bool ok = inr && v >= 0 && v < H;
-            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
-            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
+            const uint3 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint3(0, 0, 0);
         }
     };
-    auto score_col = [&](int du, const uint4 *col) {
+    auto score_col = [&](int du, const uint3 *col) {
         const int u = ex + du;
         if (u < 0 || u >= W) return;
         int64_t dd[US];
@@ -685,7 +692,7 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t s
     };
 #pragma unroll 1
     for (int du = -2 * FR; du <= 2 * FR; ++du) {
-        uint4 ca[US];
+        uint3 ca[US];
         load_col(ex + du, ey - 2 * FR, US, ca);
         score_col(du, ca);
     }
@@ -700,7 +707,7 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t s
     // ---- gather the winning window, cx-major (vFlow.cpp:923-930), into LDS
     const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
     uint64_t vis = 0;
-    auto gather_col = [&](int cxo, const uint4 *col) {
+    auto gather_col = [&](int cxo, const uint3 *col) {
         const int u = bi + cxo - FR;
 #pragma unroll
         for (int cyo = 0; cyo < side; ++cyo) {
@@ -712,7 +719,7 @@ __device__ __forceinline__ void fit_event_fast(const Ctx &c, int4 fd, uint32_t s
     };
 #pragma unroll 1
     for (int cxo = 0; cxo < side; ++cxo) {
-        uint4 ga[side];
+        uint3 ga[side];
         load_col(bi - FR + cxo, bj - FR, side, ga);
         gather_col(cxo, ga);
     }
@@ -953,7 +960,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
         any |= wok[w];
     }
     if (!any) return;  // uniform over the quad
-    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+    auto load_col = [&](int u0, int v0, int len, uint3 *col) {
         const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
         const int cbase = (u0 - c.X0) * H + v0;
 #pragma unroll
@@ -962,14 +969,14 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
             // unconditional load from a clamped index, then select: a load under a
             // branch is waited for at the branch's end, serializing the column
             const bool ok = inr && v >= 0 && v < H;
-            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
-            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
+            const uint3 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint3(0, 0, 0);
         }
     };
     // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
 #pragma unroll 1
     for (int du = -2 * FR + j; du <= 2 * FR; du += 4) {
-        uint4 col[US];
+        uint3 col[US];
         load_col(ex + du, ey - 2 * FR, US, col);
         const int u = ex + du;
         if (u < 0 || u >= W) continue;
@@ -1011,7 +1018,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
     uint64_t vis = 0;
 #pragma unroll 1
     for (int cxo = j; cxo < side; cxo += 4) {
-        uint4 col[side];
+        uint3 col[side];
         load_col(bi - FR + cxo, bj - FR, side, col);
         const int u = bi + cxo - FR;
 #pragma unroll
@@ -1125,7 +1132,7 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
         any |= wok[w];
     }
     if (!any) return;  // uniform over the quad
-    auto load_col = [&](int u0, int v0, int len, uint4 *col) {
+    auto load_col = [&](int u0, int v0, int len, uint3 *col) {
         const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
         const int cbase = (u0 - c.X0) * H + v0;
 #pragma unroll
@@ -1134,8 +1141,8 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
             // unconditional load from a clamped index, then select: a load under a
             // branch is waited for at the branch's end, serializing the column
             const bool ok = inr && v >= 0 && v < H;
-            const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
-            col[i] = ok ? hd : make_uint4(0, 0, 0, 0);
+            const uint3 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+            col[i] = ok ? hd : make_uint3(0, 0, 0);
         }
     };
     // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
@@ -1145,7 +1152,7 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     for (int sl = 0; sl < NC; ++sl) {  // unrolled: the loads of every column are in flight together
         const int du = -2 * FR + j + 4 * sl;
         if (du > 2 * FR) continue;
-        uint4 col[US];
+        uint3 col[US];
         load_col(ex + du, ey - 2 * FR, US, col);
         const int u = ex + du;
         if (u < 0 || u >= W) continue;
@@ -1316,7 +1323,7 @@ __device__ __forceinline__ void fit_event_quad_r(const Ctx &c, int4 fd, uint32_t
     const int v0 = ey - 2 * FR;
 #pragma unroll 1
     for (int cb = 0; cb < US; cb += 3) {  // three union columns at a time: their loads in flight together
-        uint4 col[3][NR];
+        uint3 col[3][NR];
 #pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
             const int ucol = cb + cc;
@@ -1329,8 +1336,8 @@ __device__ __forceinline__ void fit_event_quad_r(const Ctx &c, int4 fd, uint32_t
                 // unconditional load from a clamped index, then select (a load
                 // under a branch is waited for at the branch end)
                 const bool ok = inr && i < US && v >= 0 && v < H;
-                const uint4 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
-                col[cc][r] = ok ? hd : make_uint4(0, 0, 0, 0);
+                const uint3 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
+                col[cc][r] = ok ? hd : make_uint3(0, 0, 0);
             }
         }
 #pragma unroll
@@ -2392,7 +2399,7 @@ __global__ void k_seed_sae(Ctx c, const int64_t *stamp) {
     if (q >= c.WH) return;
     const int64_t s = stamp[q + (int64_t)c.X0 * c.H];
     SaeHead hd{};
-    hd.tag = s >= 0 ? 0x80000000u : 0u;  // chunk seq 0: never matches a chunk
+    hd.w = s >= 0 ? kHeadVisited : 0u;  // not touched
     hd.tsnap = s >= 0 ? (uint32_t)s : 0u;
     c.cells.head[q] = hd;  // both SAE buffers (heads are contiguous: buffer 1 follows buffer 0)
     c.cells.head[q + c.WH] = hd;
@@ -2404,7 +2411,7 @@ __global__ void k_last_time(const SaeHead *cells, int64_t WH, double *out) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= WH) return;
     const SaeHead s = cells[q];
-    out[q] = (s.tag >> 31) ? (double)s.tsnap : 0.0;
+    out[q] = (s.w & kHeadVisited) ? (double)s.tsnap : 0.0;
 }
 
 // Algorithmic-work counters for the roofline: U_loc per event,
@@ -3292,9 +3299,28 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // 113 instead of 97 ms at C3).
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    // FARMS_POOL_CU_SKIP = k (0..8, A/B aid): k CUs of every 32 left out of
+    // the pooling stream's CU mask, so that the fit chain always finds free
+    // slots there.  Word j of the mask clears bits 8 (t % 4) + (j + t) % 8, t <
+    // k: k per 32-CU word and k per residue mod 8, whichever way the bits map
+    // to the XCDs.
+    std::vector<uint32_t> pool_mask;
+    if (const char *v = getenv("FARMS_POOL_CU_SKIP")) {
+        const int k = std::max(0, std::min(atoi(v), 8));
+        int dev = 0;
+        hipDeviceProp_t dp{};
+        if (k > 0 && hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&dp, dev) == hipSuccess &&
+            dp.multiProcessorCount % 32 == 0) {
+            pool_mask.assign((size_t)dp.multiProcessorCount / 32, 0xffffffffu);
+            for (int j = 0; j < (int)pool_mask.size(); ++j)
+                for (int t = 0; t < k; ++t) pool_mask[j] &= ~(1u << (8 * (t & 3) + ((j + t) & 7)));
+        }
+    }
     if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+        (pool_mask.empty()
+             ? hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo)
+             : hipExtStreamCreateWithCUMask(&h->s_pool, (uint32_t)pool_mask.size(), pool_mask.data())) != hipSuccess ||
         hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {
@@ -3424,7 +3450,7 @@ extern "C" int farms_get_last_event_time(const farms_handle *h, double *out) {
     if (err == hipSuccess && h->first_q >= 0) {
         SaeHead cell{};
         err = hipMemcpy(&cell, h->sae_head + (h->first_q - (int64_t)h->X0 * h->H), sizeof(cell), hipMemcpyDeviceToHost);
-        if (err == hipSuccess && !(cell.tag >> 31)) out[h->first_q] = (double)h->first_t;
+        if (err == hipSuccess && !(cell.w & kHeadVisited)) out[h->first_q] = (double)h->first_t;
     }
     if (err != hipSuccess) return fail(FARMS_EHIP, std::string("farms_get_last_event_time: ") + hipGetErrorString(err));
     return FARMS_OK;
@@ -3495,7 +3521,7 @@ namespace {
 int check_device_call(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
                       const int32_t *d_p, int64_t n, const farms_records *d_out) {
     if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
-    if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
+    if (n < 0 || n > kMaxCallEvents) return fail(FARMS_EINVAL, "event count out of range (at most 2^29 - 1 per device call)");
     if (n > 0 && (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx ||
                   !d_out->vy || !d_out->r_local || !d_out->theta_local || !d_out->scale))
         return fail(FARMS_EINVAL, "null array");
@@ -3579,7 +3605,7 @@ extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const i
     if (!h || !d_out) return fail(FARMS_EINVAL, "null argument");
     if (h->prm.import_halo) return fail(FARMS_EINVAL, "an import_halo handle runs farms_fit_device / farms_pool_device");
     if (h->ph_count > 0) return fail(FARMS_EINVAL, "a farms_fit_device is waiting for farms_pool_device");
-    if (n < 0 || n >= INT_MAX) return fail(FARMS_EINVAL, "event count out of range");
+    if (n < 0 || n > kMaxCallEvents) return fail(FARMS_EINVAL, "event count out of range (at most 2^29 - 1 per device call)");
     if (n == 0) return FARMS_OK;
     if (!d_x || !d_y || !d_t || !d_p || !d_out->r_true || !d_out->theta_true || !d_out->vx || !d_out->vy ||
         !d_out->r_local || !d_out->theta_local || !d_out->scale)
@@ -3702,6 +3728,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         const int64_t per = std::max<int64_t>(4 * super, (n / nsub + super - 1) / super * super);
         if (n > 2 * per) sub = per;
     }
+    if (sub > kMaxCallEvents) sub = std::max<int64_t>(kMaxCallEvents / super, 1) * super;  // event ids of a sub-batch: 29 bits
     const int nbat = ceil_div(n, sub);
     int rc = FARMS_OK;
     for (int k = 0; k < std::min(nbat, 2) && !rc; ++k) rc = ensure_capacity(h, h->ws[k], sub);  // set b % 2

@@ -133,7 +133,9 @@ int farms_host_alloc(int64_t bytes, void **out);
 int farms_host_free(void *p);
 
 /* Same with device-resident inputs and outputs (no PCIe traffic).  Synchronous
- * with respect to the handle's stream. */
+ * with respect to the handle's stream.  At most 2^29 - 1 events per device call
+ * (FARMS_EINVAL beyond; feed longer streams in pieces: split calls are bitwise
+ * one call); farms_process cuts longer host calls itself. */
 int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y,
                          const uint32_t *d_t_rel, const int32_t *d_p, int64_t n,
                          farms_records *d_out);

@@ -209,6 +209,7 @@ struct Ctx {
     int NB, C2;            // ring size, events per pooling chunk
     int ring0;             // ring buffer of the call's first pooling chunk (chunk numbers continue across calls)
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
+    int fit_band;          // fit blocks per pooling chunk for the band block mapping (0: runs of 8 per XCD)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
     // with its pixel's lastEventTime still holding link.w, the stamp before it
@@ -255,6 +256,35 @@ __device__ __forceinline__ int64_t sae_resolve_h(const Ctx &c, uint3 h, uint32_t
     return (h.z & kHeadVisited) ? (int64_t)h.x : int64_t(-1);
 }
 
+// Head-only resolution for the deferred form (fit_event_quad_u): when the
+// tail decides (the pixel fired more than once in the chunk, its first
+// in-chunk event at or before e), *defer is set and the first in-chunk stamp
+// t1 is returned as a provisional value, which sae_fix_tail corrects after the
+// scan.  Resolving those cells in place put a dependent tail load under a
+// branch in every cell step, and the branch end waited for every load in
+// flight: one serialized round trip per cell step whenever any lane of the
+// wave needed its tail (with 131,072-event fit chunks, 16% of the touched
+// pixels fire twice).
+__device__ __forceinline__ int64_t sae_resolve_head(uint3 h, int e, bool &defer) {
+    defer = false;
+    if (h.z & kHeadTouched) {
+        const int e1 = (int)(h.z & kHeadE1Mask);
+        if (e1 <= e) {
+            defer = (h.z & kHeadMore) != 0;
+            return (int64_t)h.y;
+        }
+    }
+    return (h.z & kHeadVisited) ? (int64_t)h.x : int64_t(-1);
+}
+// The stamp as of e of a deferred cell q (its head says: touched, first event
+// at or before e, more than one in-chunk event; t1 its first stamp), from the
+// tail already loaded into g.
+__device__ __forceinline__ uint32_t sae_fix_tail(const Ctx &c, uint4 g, uint32_t t1, int e) {
+    if ((int)(g.x & kSeqMask) > e) return t1;
+    if (!(g.x >> 31)) return g.y;
+    return run_asof(c, (int)g.z, (int)g.w, e, g.y);
+}
+
 __device__ __forceinline__ uint3 sae_head(const Ctx &c, uint32_t q) {
     const SaeHead hd = c.cells.head[q];  // one dwordx3 load
     return make_uint3(hd.tsnap, hd.t1, hd.w);
@@ -286,6 +316,17 @@ __device__ __forceinline__ int xcd_block_grouped(int b, int G) {
     return (i / R) * (8 * R) + x * R + (i % R);
 }
 __device__ __forceinline__ int work_block() { return xcd_block((int)blockIdx.x, (int)gridDim.x); }
+// Band variant for the fit (FARMS_FIT_XCD=band): a fit chunk's positions are
+// pooling chunks in (8x8 tile) order, x-major, so the x-th eighth of each
+// pooling chunk's positions is a band of the sensor's columns; XCD x takes that
+// eighth of every pooling chunk (bpc blocks per pooling chunk), so that its L2
+// keeps one band of the SAE across the launch and the next ones.  Bijective on
+// [0, G) when G is a multiple of bpc and bpc of 8; other grids: runs of 8.
+__device__ __forceinline__ int xcd_band_block(int b, int G, int bpc) {
+    if (bpc <= 0 || G % bpc || bpc % 8) return xcd_block_grouped(b, G);
+    const int x = b & 7, i = b >> 3, per = bpc >> 3;
+    return (i / per) * bpc + x * per + (i % per);
+}
 
 // ---------------------------------------------------------------------------
 // prep
@@ -973,22 +1014,29 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
             col[i] = ok ? hd : make_uint3(0, 0, 0);
         }
     };
-    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
+    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union
+    // columns; cells whose tail decides take their first in-chunk stamp and
+    // are corrected after the scan (sae_resolve_head)
+    auto ddiff = [&](uint32_t tk) { return (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0); };
+    uint64_t pend = 0;  // deferred cells: bit (column slot) * US + row
 #pragma unroll 1
     for (int du = -2 * FR + j; du <= 2 * FR; du += 4) {
         uint3 col[US];
         load_col(ex + du, ey - 2 * FR, US, col);
         const int u = ex + du;
         if (u < 0 || u >= W) continue;
+        const int sl = (du + 2 * FR) >> 2;
         int64_t dd[US];
 #pragma unroll
         for (int i = 0; i < US; ++i) {
             const int v = ey + i - 2 * FR;
             dd[i] = 0;
             if (v < 0 || v >= H) continue;
-            const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
+            bool defer;
+            const int64_t st = sae_resolve_head(col[i], e, defer);
+            pend |= defer ? 1ull << (sl * US + i) : 0ull;
             const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
-            dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+            dd[i] = ddiff(tk);
         }
 #pragma unroll
         for (int ovi = 0; ovi < 3; ++ovi) {
@@ -999,6 +1047,35 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
             for (int oui = 0; oui < 3; ++oui) {
                 const int ou = (oui - 1) * FR;
                 if (du - ou <= FR && ou - du <= FR) score[oui * 3 + ovi] += sv;
+            }
+        }
+    }
+    // the deferred cells: head (its t1) and tail, four cells in flight at a time
+#pragma unroll 1
+    while (pend) {
+        int bit[4];
+        uint3 hh[4];
+        uint4 g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bit[k] = pend ? (int)__builtin_ctzll(pend) : -1;
+            pend &= pend ? pend - 1 : 0ull;
+            const int b = bit[k] < 0 ? 0 : bit[k];
+            const uint32_t q = bit[k] < 0 ? 0u : (uint32_t)((ex + j + 4 * (b / US) - 2 * FR - c.X0) * H + ey + b % US - 2 * FR);
+            hh[k] = sae_head(c, q);
+            g[k] = reinterpret_cast<const uint4 *>(c.cells.tail)[q];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (bit[k] < 0) continue;
+            const uint32_t t1 = hh[k].y, tk = sae_fix_tail(c, g[k], t1, e);
+            if (tk == t1) continue;
+            const int64_t delta = ddiff(tk) - ddiff(t1);
+            const int du = j + 4 * (bit[k] / US) - 2 * FR, i = bit[k] % US;
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                const int ou = (w / 3 - 1) * FR, ovi = w % 3;
+                if (du - ou <= FR && ou - du <= FR && i >= ovi * FR && i <= ovi * FR + 2 * FR) score[w] += delta;
             }
         }
     }
@@ -1013,20 +1090,41 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
     if (bw < 0 || best > nn * (int64_t(1) << 32)) return;  // uniform over the quad
 
     // ---- gather the winning window, cx-major (vFlow.cpp:923-930): this lane's
-    // columns into LDS (lt[k * kFitQS]), visited mask combined over the quad
+    // columns into LDS (lt[k * kFitQS]), visited mask combined over the quad;
+    // deferred cells again corrected after the pass
     const int bi = ex + (bw / 3 - 1) * FR, bj = ey + (bw % 3 - 1) * FR;
-    uint64_t vis = 0;
+    uint64_t vis = 0, pend2 = 0;
 #pragma unroll 1
     for (int cxo = j; cxo < side; cxo += 4) {
         uint3 col[side];
         load_col(bi - FR + cxo, bj - FR, side, col);
-        const int u = bi + cxo - FR;
 #pragma unroll
         for (int cyo = 0; cyo < side; ++cyo) {
             const int k = cxo * side + cyo;
-            const int64_t st = sae_resolve_h(c, col[cyo], (uint32_t)((u - c.X0) * H + bj - FR + cyo), e, seq);
+            bool defer;
+            const int64_t st = sae_resolve_head(col[cyo], e, defer);
             vis |= st >= 0 ? 1ull << k : 0ull;
+            pend2 |= defer ? 1ull << k : 0ull;
             lt[k * kFitQS] = st < 0 ? 0u : (uint32_t)st;
+        }
+    }
+#pragma unroll 1
+    while (pend2) {
+        int kk[4];
+        uint4 g[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            kk[m] = pend2 ? (int)__builtin_ctzll(pend2) : -1;
+            pend2 &= pend2 ? pend2 - 1 : 0ull;
+            const int k = kk[m] < 0 ? 0 : kk[m];
+            const uint32_t q = kk[m] < 0 ? 0u : (uint32_t)((bi + k / side - FR - c.X0) * H + bj + k % side - FR);
+            g[m] = reinterpret_cast<const uint4 *>(c.cells.tail)[q];
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            if (kk[m] < 0) continue;
+            uint32_t *slot = &lt[kk[m] * kFitQS];
+            *slot = sae_fix_tail(c, g[m], *slot, e);
         }
     }
     vis = quad_or_u64(vis);
@@ -1147,7 +1245,9 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     };
     // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
     uint64_t umask = 0;  // visited bits of this lane's union cells: (slot * US + row), slot = column / 4
+    uint64_t pend = 0;   // cells whose tail decides (sae_resolve_head): fixed after the scan
     constexpr int NC = (US + 3) / 4;  // union columns per lane (the last one absent on some lanes)
+    auto ddiff = [&](uint32_t tk) { return (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0); };
 #pragma unroll
     for (int sl = 0; sl < NC; ++sl) {  // unrolled: the loads of every column are in flight together
         const int du = -2 * FR + j + 4 * sl;
@@ -1163,11 +1263,13 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
             const int v = ey + i - 2 * FR;
             dd[i] = 0;
             if (v < 0 || v >= H) continue;
-            const int64_t st = sae_resolve_h(c, col[i], (uint32_t)((u - c.X0) * H + v), e, seq);
+            bool defer;
+            const int64_t st = sae_resolve_head(col[i], e, defer);
             const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
             ut[(ucol * US + i) * kFitQS] = tk;
             umask |= st >= 0 ? 1ull << ((ucol >> 2) * US + i) : 0ull;
-            dd[i] = (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0);
+            pend |= defer ? 1ull << ((ucol >> 2) * US + i) : 0ull;
+            dd[i] = ddiff(tk);
         }
 #pragma unroll
         for (int ovi = 0; ovi < 3; ++ovi) {
@@ -1178,6 +1280,40 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
             for (int oui = 0; oui < 3; ++oui) {
                 const int ou = (oui - 1) * FR;
                 if (du - ou <= FR && ou - du <= FR) score[oui * 3 + ovi] += sv;
+            }
+        }
+    }
+    // ---- the deferred cells: their tails, four loads in flight at a time;
+    // each corrected stamp replaces the provisional t1 in the union tile and in
+    // the scores of the windows that contain the cell (exact integers: any order)
+#pragma unroll 1
+    while (pend) {
+        int bit[4];
+        uint4 g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bit[k] = pend ? (int)__builtin_ctzll(pend) : -1;
+            pend &= pend ? pend - 1 : 0ull;
+            const int b = bit[k] < 0 ? 0 : bit[k];
+            const int ucol = j + 4 * (b / US), i = b % US;
+            const uint32_t q = (uint32_t)((ex + ucol - 2 * FR - c.X0) * H + ey + i - 2 * FR);
+            g[k] = reinterpret_cast<const uint4 *>(c.cells.tail)[bit[k] < 0 ? 0u : q];  // e2m, t2, run_lo, run_hi
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (bit[k] < 0) continue;
+            const int ucol = j + 4 * (bit[k] / US), i = bit[k] % US;
+            uint32_t *slot = &ut[(ucol * US + i) * kFitQS];
+            const uint32_t t1 = *slot;
+            const uint32_t tk = sae_fix_tail(c, g[k], t1, e);
+            if (tk == t1) continue;
+            *slot = tk;
+            const int64_t delta = ddiff(tk) - ddiff(t1);
+            const int du = ucol - 2 * FR;
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                const int ou = (w / 3 - 1) * FR, ovi = w % 3;
+                if (du - ou <= FR && ou - du <= FR && i >= ovi * FR && i <= ovi * FR + 2 * FR) score[w] += delta;
             }
         }
     }
@@ -1490,11 +1626,14 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
         return;
     }
     const int bid = (int)blockIdx.x;
+#ifdef FARMS_FIT_VFLOOR  // tuning builds (make variant DEFS=-DFARMS_FIT_VFLOOR=\"v79\"): a VGPR floor for the fit
+    asm volatile("" ::: FARMS_FIT_VFLOOR);
+#endif
     constexpr int NPC = MODE ? (4 * FR + 1) * (4 * FR + 1) : (2 * FR + 1) * (2 * FR + 1);
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
     // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
-    const int fb = xcd_block_grouped(bid, G);
+    const int fb = xcd_band_block(bid, G, c.fit_band);
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -1729,7 +1868,10 @@ __device__ __forceinline__ ChainFlow chain_load(const FlowCell *p) {
 }
 // One-wave workgroups (a 4-wave one needs 4 x 128 VGPRs free at once on one
 // CU, which the pooling waves rarely leave), at most 128 VGPRs (4 waves per SIMD).
-__global__ __launch_bounds__(64, 4) void k_chain(Ctx c, int ch0, int ch1) {
+#ifndef FARMS_CHAIN_WAVES  // tuning builds: k_chain's minimum waves per SIMD (VGPR budget)
+#define FARMS_CHAIN_WAVES 4
+#endif
+__global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0, int ch1) {
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x;
     if (g >= c.nblk) return;
@@ -2856,6 +2998,11 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.ring0 = (int)(h->chunk_base % h->NB);
+    {  // FARMS_FIT_XCD=band: the fit's blocks by sensor band per XCD (xcd_band_block)
+        const char *fx = getenv("FARMS_FIT_XCD");
+        const int bpc = h->pool_chunk / kFitQS;
+        c.fit_band = fx && fx[0] == 'b' && h->pool_chunk % kFitQS == 0 ? bpc : 0;
+    }
     const int span = 2 * h->M + 1;  // pooling window rows and columns
     c.pool_bw = (span * span + 63) / 64 + 1;  // flattened window positions (+1: a two-half step reads a word ahead)
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
@@ -3283,6 +3430,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     {
+        // FARMS_TILE_SHIFT (2..5, A/B aid): log2 of the work-order tile's edge
+        if (const char *ts = getenv("FARMS_TILE_SHIFT")) h->tile_shift = std::max(2, std::min(atoi(ts), 5));
         const int tm = (1 << h->tile_shift) - 1;
         const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);
         while ((int64_t(1) << h->tile_bits) < tiles) ++h->tile_bits;

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for CFG in ${CFGS:-3 4}; do
   for C in ${COMBOS:--}; do
-    tag=$(echo "$C" | tr ',=' '_-')
+    tag=$(echo "$C" | tr ',=/' '_-_')
     envs=()
     [ "$C" != "-" ] && IFS=',' read -ra envs <<< "$C"
     timeout -k 10 300 env "${envs[@]}" python3 bench.py --config $CFG --steps ${STEPS:-6} --warmup 2 \

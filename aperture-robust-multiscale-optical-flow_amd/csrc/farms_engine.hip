@@ -133,7 +133,8 @@ struct SaeBuf {
 constexpr uint32_t kCandMore = 0x80000000u;     // > 1 event at the cell in the chunk
 constexpr uint32_t kCandSnapOk = 0x40000000u;   // L_snap > 0
 constexpr uint32_t kCandOneOk = 0x20000000u;    // L1 > 0
-constexpr uint32_t kCandLinMask = 0x1FFFFFFFu;  // x-major cell index (W*H < 2^29)
+constexpr uint32_t kCandMore2 = 0x10000000u;    // > 2 events at the cell in the chunk
+constexpr uint32_t kCandLinMask = 0x0FFFFFFFu;  // x-major cell index (W*H < 2^28)
 struct __attribute__((aligned(16))) CandHdr {
     uint32_t lin;  // cell index | flags above
     int32_t e1;    // first in-chunk event at the cell, INT_MAX if untouched
@@ -150,7 +151,11 @@ struct __attribute__((aligned(16))) BmWord {
 struct CandVal {
     double L_snap, Lc_snap, Ls_snap;
     double L1, Lc1, Ls1;
-    int32_t run_lo, run_hi;  // the cell's in-chunk run in P (used when it has > 1 event)
+    // kCandMore2: the cell's in-chunk run [run_lo, run_hi] in P (a run search
+    // resolves the state as of an event); exactly two in-chunk events: the
+    // second one inline, run_lo = its event id | (its L > 0) << 31, run_hi = its
+    // stamp, so that one dependent load replaces the search's three
+    int32_t run_lo, run_hi;
 };
 
 constexpr uint32_t kSeqMask = 0x7FFFFFFFu;
@@ -1881,14 +1886,18 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
     int k[kChainCells], kend[kChainCells], nxt[kChainCells], pnx[kChainCells];
     ChainFlow snap[kChainCells], pf[kChainCells];
     uint32_t dirty = 0;
-    auto prefetch = [&](int i) {  // the next touch of cell i: its flow and the run entry after it
-        pnx[i] = INT_MAX;
-        pf[i] = ChainFlow{0.0, 0.0, 0.0, 0u};
-        if (nxt[i] < lim) {
-            pf[i] = chain_load(&c.evf[nxt[i]]);
-            if (k[i] + 1 <= kend[i]) pnx[i] = c.P[k[i] + 1];
-        }
+    // the next touch of cell i: its flow (read only when nxt[i] < lim) and the
+    // run entry after it (pnx(i) applies the run's end).  Loaded for every lane
+    // and cell slot after each chunk, from clamped indices, with no select on the
+    // loaded values: a load under a branch is waited for at the branch end, and
+    // a select right after the load waits for it too -- either serialized one
+    // round trip per cell slot and chunk; these stay in flight until the next
+    // chunk reads them (a cell that did not move reloads the same values).
+    auto prefetch = [&](int i) {
+        pf[i] = chain_load(&c.evf[nxt[i] < lim ? nxt[i] : 0]);
+        pnx[i] = c.P[k[i] + 1 <= kend[i] ? k[i] + 1 : 0];
     };
+    auto pnext = [&](int i) { return k[i] + 1 <= kend[i] ? pnx[i] : INT_MAX; };
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) {
         const int64_t q = (g * kChainCells + i) * 64 + lane;
@@ -1932,7 +1941,7 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
             // one, or any of a longer run)
             const int64_t ts = (int64_t)snap[i].t;
             const bool bit = (snap[i].L > 0 && ts > lo && ts < hi) ||
-                             (nxt[i] < ce && (pf[i].L > 0 || pnx[i] < ce));
+                             (nxt[i] < ce && (pf[i].L > 0 || pnext(i) < ce));
             bal[i] = __ballot(bit);
             woff[i] = acc;
             acc += (uint32_t)__popcll(bal[i]);
@@ -1951,7 +1960,7 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
             const int e1 = touched ? nxt[i] : INT_MAX;
             // one walk over the cell's in-chunk run (a longer run is rare): its last
             // position and event, and the run entry after the chunk
-            int run_hi = k1, last = e1, nn = pnx[i];
+            int run_hi = k1, last = e1, nn = pnext(i);
             if (touched) {
                 while (nn < ce) {
                     ++run_hi;
@@ -1959,6 +1968,9 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
                     nn = run_hi + 1 <= kend[i] ? c.P[run_hi + 1] : INT_MAX;
                 }
             }
+            // the last in-chunk event's flow: the next snapshot, and (a run of two)
+            // the second event inlined in the candidate record
+            const ChainFlow fl = touched && last != e1 ? chain_load(&c.evf[last]) : pf[i];
             if ((bal[i] >> lane) & 1) {  // candidate record: snapshot before ch, first in-chunk flow, run bounds
                 CandHdr hd;
                 CandVal v;
@@ -1967,10 +1979,16 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
                 v.L_snap = snap[i].L; v.Lc_snap = snap[i].Lc; v.Ls_snap = snap[i].Ls;
                 if (touched) {
                     hd.e1 = e1;
-                    hd.lin |= (run_hi > k1 ? kCandMore : 0u) | (pf[i].L > 0 ? kCandOneOk : 0u);
+                    hd.lin |= (run_hi > k1 ? kCandMore : 0u) | (run_hi > k1 + 1 ? kCandMore2 : 0u) |
+                              (pf[i].L > 0 ? kCandOneOk : 0u);
                     hd.t1 = pf[i].t;
                     v.L1 = pf[i].L; v.Lc1 = pf[i].Lc; v.Ls1 = pf[i].Ls;
-                    v.run_lo = k1; v.run_hi = run_hi;
+                    if (run_hi == k1 + 1) {  // two events: the second inline
+                        v.run_lo = (int32_t)((uint32_t)last | (fl.L > 0 ? 0x80000000u : 0u));
+                        v.run_hi = (int32_t)fl.t;
+                    } else {
+                        v.run_lo = k1; v.run_hi = run_hi;
+                    }
                 } else {
                     hd.e1 = INT_MAX;
                     hd.t1 = 0;
@@ -1981,14 +1999,16 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
                 c.hdr_ring[kb] = hd;
                 c.val_ring[kb] = v;
             }
-            if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
-                snap[i] = last != e1 ? chain_load(&c.evf[last]) : pf[i];
+            if (touched) {  // advance: snapshot <- last event of the chunk at q
+                snap[i] = fl;
                 k[i] = run_hi + 1;
                 nxt[i] = nn;
                 dirty |= 1u << i;
-                prefetch(i);
             }
         }
+        // the next touches, every slot's loads in flight together
+#pragma unroll
+        for (int i = 0; i < kChainCells; ++i) prefetch(i);
     }
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) {
@@ -2298,7 +2318,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 bool ok;
                 if (hd.e1 > e) { ok = (hd.lin & kCandSnapOk) != 0; tq = hd.t_snap; vp[h] = &cval[kc[h]].L_snap; }
                 else if (!(hd.lin & kCandMore)) { ok = (hd.lin & kCandOneOk) != 0; tq = hd.t1; vp[h] = &cval[kc[h]].L1; }
-                else {  // several events at the cell inside the chunk: search its run
+                else if (!(hd.lin & kCandMore2)) {  // two events at the cell inside the chunk: the second inline
+                    const int2 r2 = *reinterpret_cast<const int2 *>(&cval[kc[h]].run_lo);
+                    const int e2 = r2.x & 0x7FFFFFFF;
+                    if (e2 > e) { ok = (hd.lin & kCandOneOk) != 0; tq = hd.t1; vp[h] = &cval[kc[h]].L1; }
+                    else { ok = r2.x < 0; tq = (uint32_t)r2.y; vp[h] = &c.evf[e2].L; }
+                }
+                else {  // more events at the cell inside the chunk: search its run
                     const CandVal &cv = cval[kc[h]];
                     const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
                     const FlowCell fe = c.evf[sev];

@@ -182,6 +182,7 @@ struct Ctx {
     bool fit_all;          // fit_lo / fit_hi cover the stored region (no per-event test)
     int fr, min_inl, J, M;
     float invJ;            // 1/J: scale index of a cell = floor((d + J - 1 + 0.5) * invJ)
+    uint32_t kmagic;       // ceil(2^32 / J) (J > 1): ceil(d / J) = umulhi(d + J - 1, kmagic)
     const int32_t *x, *y, *p;
     const uint32_t *t;
     const uint32_t *pix;   // x*H + y per event
@@ -2293,8 +2294,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     if (total > 0) {
         locate(0, rc, kc);
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
-            if (64 * h + lane < total) hc[h] = chdr[kc[h]];
+        for (int h = 0; h < NH; ++h) hc[h] = chdr[64 * h + lane < total ? kc[h] : 0];  // (clamped: no exec mask)
     }
     // the previous step's contributors: ballots, values, smallest scales
     uint64_t pbal[NH];
@@ -2334,11 +2334,14 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115), exact on integers
                 const int64_t dt = (int64_t)teu - (int64_t)tq;
                 const int i = row_i0 + rc[h];
-                const int j = (int)(hd.lin & kCandLinMask) + OFF - i * H;
+                // (i * H < 2^24: the full-rate 24-bit multiply)
+                const int j = (int)(hd.lin & kCandLinMask) + OFF - (int)__umul24((uint32_t)i, (uint32_t)H);
                 if (ok && (uint64_t)(dt + 499) < 999u) {
                     const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
                     const int d = di > dj ? di : dj;
-                    k0[h] = (int)(((float)(d + J - 1) + 0.5f) * c.invJ);  // smallest scale containing the cell: ceil(d / J)
+                    // smallest scale containing the cell, ceil(d / J), by a multiply-high with
+                    // ceil(2^32 / J) (exact for d + J < 2^16; J = 1: d)
+                    k0[h] = J == 1 ? d : (int)__umulhi((uint32_t)(d + J - 1), c.kmagic);
                     con[h] = true;
                 }
             }
@@ -2351,14 +2354,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 #pragma unroll
         for (int h = 0; h < NH; ++h) { v[h][0] = vp[h][0]; v[h][1] = vp[h][1]; v[h][2] = vp[h][2]; }
         int rn[NH], kn[NH];
-        CandHdr hn[NH];
+        CandHdr hn[NH];  // (past the last step: the current headers, never read)
 #pragma unroll
-        for (int h = 0; h < NH; ++h) { rn[h] = 0; kn[h] = 0; hn[h] = CandHdr{}; }
-        if (f0 + 64 * NH < total) {
+        for (int h = 0; h < NH; ++h) { rn[h] = 0; kn[h] = 0; hn[h] = hc[h]; }
+        if (f0 + 64 * NH < total) {  // (wave-uniform)
             locate(f0 + 64 * NH, rn, kn);
 #pragma unroll
-            for (int h = 0; h < NH; ++h)
-                if (f0 + 64 * (NH + h) + lane < total) hn[h] = chdr[kn[h]];
+            for (int h = 0; h < NH; ++h) hn[h] = chdr[f0 + 64 * (NH + h) + lane < total ? kn[h] : 0];  // (clamped)
         }
         // ---- stage and fold the previous step's contributors
         uint64_t pany = 0;
@@ -3013,6 +3015,7 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.fit_all = c.fit_lo <= h->X0 && c.fit_hi >= h->X0 + h->WR;
     c.fr = h->fr; c.min_inl = h->prm.min_inliers; c.J = h->J; c.M = h->M;
     c.invJ = 1.0f / (float)h->J;
+    c.kmagic = h->J > 1 ? (uint32_t)(((uint64_t(1) << 32) + (uint64_t)h->J - 1) / (uint64_t)h->J) : 0u;
     c.x = dx; c.y = dy; c.t = dt; c.p = dp;
     c.pix = w.pix; c.skey = w.skey; c.P = w.P; c.link = w.link;
     c.Q = w.Q; c.qe = w.qe; c.fdesc = w.fdesc; c.plane = w.plane;

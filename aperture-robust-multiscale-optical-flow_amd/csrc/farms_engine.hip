@@ -2035,6 +2035,14 @@ __device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, i
     return lo;
 }
 
+// Element i of an array whose byte offsets fit 32 bits, addressed as a
+// wave-uniform base plus a zero-extended 32-bit offset (the global_load saddr
+// form: one VGPR of offset instead of a sign-extended 64-bit address per lane).
+template <class T>
+__device__ __forceinline__ const T &at32(const T *base, uint32_t i) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
 // Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
 // 16-lane row, then the row broadcasts of lanes 15 and 31.
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -2178,7 +2186,7 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         hi1_[hh] = l1;
         const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
                   wc = min(max(l1 >> 6, 0), wmax);
-        const BmWord A = bwb[wa], B = bwb[wb], C = bwb[wc];
+        const BmWord A = at32(bwb, (uint32_t)wa), B = at32(bwb, (uint32_t)wb), C = at32(bwb, (uint32_t)wc);
         bA[hh] = A.bm; oA[hh] = A.wo;
         bB[hh] = B.bm; oB[hh] = B.wo;
         bC[hh] = C.bm; oC[hh] = C.wo;
@@ -2294,7 +2302,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     if (total > 0) {
         locate(0, rc, kc);
 #pragma unroll
-        for (int h = 0; h < NH; ++h) hc[h] = chdr[64 * h + lane < total ? kc[h] : 0];  // (clamped: no exec mask)
+        for (int h = 0; h < NH; ++h) hc[h] = at32(chdr, 64 * h + lane < total ? (uint32_t)kc[h] : 0u);  // (clamped: no exec mask)
     }
     // the previous step's contributors: ballots, values, smallest scales
     uint64_t pbal[NH];
@@ -2360,7 +2368,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         if (f0 + 64 * NH < total) {  // (wave-uniform)
             locate(f0 + 64 * NH, rn, kn);
 #pragma unroll
-            for (int h = 0; h < NH; ++h) hn[h] = chdr[f0 + 64 * (NH + h) + lane < total ? kn[h] : 0];  // (clamped)
+            for (int h = 0; h < NH; ++h) hn[h] = at32(chdr, f0 + 64 * (NH + h) + lane < total ? (uint32_t)kn[h] : 0u);  // (clamped)
         }
         // ---- stage and fold the previous step's contributors
         uint64_t pany = 0;

@@ -194,12 +194,15 @@ def kernel_roofline(cfg: int, split: str, kernel: str, kname: str, launches: int
     if sq and avg_us > 0:
         waves = max(sq["SQ_WAVES"], 1.0)
         wave_cyc = max(sq["SQ_WAVE_CYCLES"], 1.0)
-        # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; a wave64
-        # VALU instruction occupies a SIMD-32 for 2 of them (fp64: 4), so this
-        # utilisation is a lower bound of the VALU pipe's busy fraction
+        # SIMD-cycles the launch had: 1,024 SIMDs x 2.4 GHz x duration; one wave's
+        # stream of independent wave64 VALU instructions issues one per 4 cycles
+        # on its SIMD (v_add_f32 / v_fma_f32, /opt/skills/guides/MI355X_MICROARCH.md
+        # per-instruction table), so this is the fraction of the launch's SIMD
+        # cycles its VALU instructions occupy (the PMC pass runs kernels alone;
+        # the duration is the concurrent one, so it reads low)
         simd_cycles = 1024 * 2.4e9 * avg_us * 1e-6
         r["issue"] = {"valu_insts_per_wave": round(sq["SQ_INSTS_VALU"] / waves, 1),
-                      "valu_issue_util": round(2.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
+                      "valu_issue_util": round(4.0 * sq["SQ_INSTS_VALU"] / simd_cycles, 4),
                       "wait_any_frac": round(sq["SQ_WAIT_ANY"] / wave_cyc, 4),
                       "wait_inst_frac": round(sq["SQ_WAIT_INST_ANY"] / wave_cyc, 4),
                       "active_inst_frac": round(sq["SQ_ACTIVE_INST_ANY"] / wave_cyc, 4),

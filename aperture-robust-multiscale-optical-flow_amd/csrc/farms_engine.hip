@@ -217,6 +217,16 @@ struct Ctx {
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
     int fit_band;          // fit blocks per pooling chunk for the band block mapping (0: runs of 8 per XCD)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
+    // event-driven candidate build (k_cand): per pooling chunk the first chunk
+    // whose events can still be snapshots inside its kill window (cbk), the
+    // call-start snapshot list {cell, stamp, first event of the call at the
+    // cell}, the call's plan (kCi* below) and the per-(chunk, slice) scratch of
+    // candidate items
+    const int32_t *cbk;
+    const int4 *slist;
+    int *cinfo;
+    int32_t *cscr;
+    int cgps, cslices;     // candidate groups per slice, slices
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
     // with its pixel's lastEventTime still holding link.w, the stamp before it
     // (written only after pooling, :790)
@@ -1838,6 +1848,22 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
 // chain waves take slots from the fit and pooling, fewer lengthen the chain.
 constexpr int kGroupCells = 256;
 
+// The call's candidate-build plan (Ctx::cinfo, per workspace set):
+//   kCiFlag     1: k_cand builds the candidate lists, 0: k_chain does
+//   kCiMaxBack  largest chunk distance back to cbk (k_cand_plan_back)
+//   kCiCount    call-start snapshot list length (k_cand_list)
+//   kCiLMin/Max stamp range of that list
+//   kCiTMin/Max stamp range of the call's events
+enum { kCiFlag = 0, kCiMaxBack, kCiCount, kCiLMin, kCiLMax, kCiTMin, kCiTMax, kCiWords };
+// k_cand takes a call when every chunk's kill window reaches back at most this
+// many chunks (a time-ordered stream: 2-3) and the call-start snapshot list
+// inside the call's stamp span is at most kCandMaxList cells; other streams
+// (out-of-order stamps) keep k_chain, whose cost is independent of the order.
+constexpr int kCandMaxBack = 64;
+constexpr int kCandMaxList = 1 << 18;
+constexpr int kCandThreads = 512;
+constexpr int kCandSliceGroups = 1024;  // candidate groups per k_cand slice at most (32 KB of LDS bitmap)
+
 
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling
 // chunks [ch0, ch1)).  A wavefront owns one candidate group (kGroupCells = 256
@@ -1881,6 +1907,7 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x;
     if (g >= c.nblk) return;
+    if (c.cinfo[kCiFlag]) return;  // k_cand builds this call's candidates
     const int n = c.n, C2 = c.C2;
     const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
     const uint64_t lt = (1ull << lane) - 1;
@@ -2022,6 +2049,321 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
             c.pcur[q] = k[i];
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Event-driven candidate build (k_cand): the same candidate lists as k_chain,
+// from the events instead of a sweep over every cell.  k_chain keeps each
+// cell's state in registers across a super-chunk's 64 chunks, one wave per
+// 256 cells for the whole launch: 3,600 waves of 128 VGPRs at 1280 x 720,
+// mostly waiting on one dependent round trip per chunk, while ~31% of the
+// cells fire in a super-chunk and ~2% are candidates of a chunk.  Here the
+// candidates of chunk ch = [cs, ce) come from three disjoint sources:
+//   S1  the first event e at each cell touched in ch (link prev < cs): its
+//       snapshot is the flow of the previous event at the cell (link prev),
+//       or the call-start snapshot fsnap when the call had none;
+//   S2  an earlier event e' of the call that is the last at its cell before ce
+//       (link next >= ce) with valid flow and stamp inside the chunk's kill
+//       window -- only chunks [cbk[ch], ch) can hold one (cbk from the prefix
+//       maximum of the chunks' last stamps);
+//   S3  a cell of the call-start snapshot list (valid snapshot flow) whose
+//       stamp is inside the kill window and whose first event of the call is
+//       at or past ce.
+// bit(q) is k_chain's: S1 cells when the cell fires more than once in ch, its
+// first flow is valid, or its snapshot is valid and inside the window; S2/S3
+// cells always.  So the bitmap words and the records are k_chain's, the
+// candidate slot of a cell is its rank in cell order inside its group, and
+// k_pool reads the same lists.  Chunks are independent: one workgroup per
+// (chunk, slice of the sensor's groups) marks its cells in an LDS bitmap,
+// writes the words with their group-local offsets, then the records.
+// fsnap holds the call-start snapshots while the call runs; k_cand_commit
+// advances it to each cell's last event once the call's lists are built.
+
+// Prefix maximum of the chunks' last stamps and the call's stamp span (one block).
+__global__ __launch_bounds__(1024) void k_cand_plan_max(const uint32_t *tmin, const uint32_t *tmax, int nch,
+                                                        uint32_t *pmax, int *info) {
+    __shared__ uint32_t smax[1024], smin[1024];
+    const int T = (int)blockDim.x, tid = (int)threadIdx.x;
+    const int per = (nch + T - 1) / T;
+    const int a = min(tid * per, nch), b = min(a + per, nch);
+    uint32_t m = 0, mn = 0xFFFFFFFFu;
+    for (int i = a; i < b; ++i) {
+        m = max(m, tmax[i]);
+        mn = min(mn, tmin[i]);
+    }
+    smax[tid] = m;
+    smin[tid] = mn;
+    __syncthreads();
+    for (int off = 1; off < T; off <<= 1) {  // inclusive max-scan over the threads' segments
+        const uint32_t v = tid >= off ? smax[tid - off] : 0u;
+        __syncthreads();
+        smax[tid] = max(smax[tid], v);
+        __syncthreads();
+    }
+    uint32_t run = tid > 0 ? smax[tid - 1] : 0u;
+    for (int i = a; i < b; ++i) {
+        run = max(run, tmax[i]);
+        pmax[i] = run;
+    }
+    for (int s = T / 2; s > 0; s >>= 1) {
+        if (tid < s) smin[tid] = min(smin[tid], smin[tid + s]);
+        __syncthreads();
+    }
+    if (tid == 0) {
+        info[kCiFlag] = 0;
+        info[kCiMaxBack] = 0;
+        info[kCiCount] = 0;
+        info[kCiLMin] = (int)0xFFFFFFFFu;
+        info[kCiLMax] = 0;
+        info[kCiTMin] = (int)smin[0];
+        info[kCiTMax] = (int)smax[T - 1];
+    }
+}
+
+// cbk[ch]: the first chunk c' < ch whose prefix-maximum last stamp is inside
+// ch's kill window (no event of an earlier chunk can be a snapshot candidate
+// of ch: its stamp is <= tmin - 500); ch if none.
+__global__ void k_cand_plan_back(const uint32_t *tmin, const uint32_t *pmax, int nch, int32_t *bk, int *info) {
+    const int ch = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (ch >= nch) return;
+    const int64_t lo = (int64_t)tmin[ch] - (int64_t)kKillUs;
+    int a = 0, b = ch;
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if ((int64_t)pmax[m] > lo) b = m;
+        else a = m + 1;
+    }
+    bk[ch] = a;
+    atomicMax(&info[kCiMaxBack], ch - a);
+}
+
+// The call-start snapshot list: cells whose snapshot flow is valid with a stamp
+// inside the call's span widened by the kill time, with the first event of the
+// call at the cell (INT_MAX: none).  Any order (k_cand's bitmap ranks them).
+__global__ void k_cand_list(Ctx c, int4 *list) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int *info = c.cinfo;
+    const int lane = (int)(threadIdx.x & 63);
+    bool keep = false;
+    int4 ent = make_int4(0, 0, 0, 0);
+    if (q < c.WH) {
+        const int64_t ft = c.ftime[q];
+        const int64_t lo = (int64_t)(uint32_t)info[kCiTMin] - (int64_t)kKillUs,
+                      hi = (int64_t)(uint32_t)info[kCiTMax] + (int64_t)kKillUs;
+        if (ft >= 0 && ft > lo && ft < hi) {
+            keep = true;
+            const int first = c.pend[q] >= 0 ? c.P[c.pcur[q]] : INT_MAX;
+            ent = make_int4((int)q, (int)(uint32_t)ft, first, 0);
+        }
+    }
+    const uint64_t bal = __ballot(keep);
+    if (!bal) return;
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&info[kCiCount], (int)__popcll(bal));
+    base = __shfl(base, leader, 64);
+    if (keep) {
+        const int i = base + (int)__popcll(bal & ((1ull << lane) - 1));
+        if (i < kCandMaxList) list[i] = ent;  // a longer list hands the call to k_chain
+        atomicMin(reinterpret_cast<unsigned int *>(&info[kCiLMin]), (unsigned int)ent.y);
+        atomicMax(reinterpret_cast<unsigned int *>(&info[kCiLMax]), (unsigned int)ent.y);
+    }
+}
+
+// force: 0 by the stream, 1 k_cand (unless the list overflowed), 2 k_chain
+// (FARMS_CAND, A/B and test aid).
+__global__ void k_cand_flag(int *info, int force) {
+    const bool fits = info[kCiCount] <= kCandMaxList;  // the list holds every call-start snapshot needed
+    const bool local = info[kCiMaxBack] <= kCandMaxBack;
+    info[kCiFlag] = fits && force != 2 && (force == 1 || local) ? 1 : 0;
+}
+
+// One workgroup per (pooling chunk, slice of cgps candidate groups) of chunks
+// [ch0, ch1).
+__global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) {
+    if (!c.cinfo[kCiFlag]) return;  // k_chain builds this call's candidates
+    extern __shared__ uint64_t s_bm[];  // the slice's bitmap words
+    __shared__ int s_cnt;
+    const int lb = work_block();  // XCD-contiguous: the slices of a chunk share an L2
+    const int ch = ch0 + lb / c.cslices, sl = lb % c.cslices;
+    if (ch >= ch1) return;
+    const int tid = (int)threadIdx.x, T = (int)blockDim.x, lane = tid & 63;
+    const int g0 = sl * c.cgps, g1 = min(g0 + c.cgps, c.nblk);
+    if (g0 >= g1) return;
+    const uint32_t qa = (uint32_t)g0 * kGroupCells, qb = (uint32_t)min((int64_t)g1 * kGroupCells, c.WH);
+    const int nw = (g1 - g0) * 4;
+    for (int i = tid; i < nw; i += T) s_bm[i] = 0;
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    const int n = c.n, C2 = c.C2;
+    const int cs = ch * C2, ce = min(cs + C2, n);
+    const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
+    const int cap = c.cgps * kGroupCells;
+    int32_t *scr = c.cscr + ((int64_t)(ch - ch0) * c.cslices + sl) * (int64_t)cap;
+    const uint64_t lt = (1ull << lane) - 1;
+    // mark q, keep the item (wave-aggregated slot claim)
+    auto push = [&](bool keep, uint32_t q, int item) {
+        const uint64_t bal = __ballot(keep);
+        if (!bal) return;
+        const int leader = __ffsll((unsigned long long)bal) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&s_cnt, (int)__popcll(bal));
+        base = __shfl(base, leader, 64);
+        if (keep) {
+            atomicOr((unsigned long long *)&s_bm[(q - qa) >> 6], 1ull << (q & 63));
+            const int i = base + (int)__popcll(bal & lt);
+            if (i < cap) scr[i] = item;  // (a cell is an item at most once: i < cap always)
+        }
+    };
+    // S1: first events of the chunk at their cells
+    for (int e0 = cs; e0 < ce; e0 += T) {
+        const int e = e0 + tid;
+        bool keep = false;
+        uint32_t q = 0;
+        if (e < ce) {
+            q = c.pix[e];
+            if (q >= qa && q < qb) {
+                const int4 lk = c.link[e];
+                if (lk.y < cs) {
+                    if (lk.z < ce) keep = true;
+                    else {
+                        const FlowCell *sp = lk.y >= 0 ? &c.evf[lk.y] : &c.fsnap[q];
+                        const double Le = c.evf[e].L, Ls = sp->L;
+                        const int64_t ts = (int64_t)sp->t;
+                        keep = Le > 0 || (Ls > 0 && ts > lo && ts < hi);
+                    }
+                }
+            }
+        }
+        push(keep, q, e);
+    }
+    // S2: the last events before the chunk at untouched cells, from the chunks
+    // whose stamps reach the kill window
+    for (int cp = c.cbk[ch]; cp < ch; ++cp) {
+        if (!((int64_t)c.ctmax[cp] > lo && (int64_t)c.ctmin[cp] < hi)) continue;
+        const int a = cp * C2, b = min(a + C2, n);
+        for (int e0 = a; e0 < b; e0 += T) {
+            const int e = e0 + tid;
+            bool keep = false;
+            uint32_t q = 0;
+            if (e < b) {
+                const int64_t te = (int64_t)c.t[e];
+                if (te > lo && te < hi) {
+                    q = c.pix[e];
+                    if (q >= qa && q < qb && c.link[e].z >= ce) keep = c.evf[e].L > 0;
+                }
+            }
+            push(keep, q, e);
+        }
+    }
+    // S3: call-start snapshots of cells the call has not touched before ce
+    {
+        const int cnt = c.cinfo[kCiCount];
+        if (cnt > 0 && (int64_t)(uint32_t)c.cinfo[kCiLMax] > lo && (int64_t)(uint32_t)c.cinfo[kCiLMin] < hi) {
+            for (int i0 = 0; i0 < cnt; i0 += T) {
+                const int i = i0 + tid;
+                bool keep = false;
+                uint32_t q = 0;
+                if (i < cnt) {
+                    const int4 en = c.slist[i];
+                    q = (uint32_t)en.x;
+                    const int64_t ft = (int64_t)(uint32_t)en.y;
+                    keep = q >= qa && q < qb && ft > lo && ft < hi && en.z >= ce;
+                }
+                push(keep, q, ~(int)q);
+            }
+        }
+    }
+    __syncthreads();
+    // bitmap words with the group-local offset of their first candidate
+    const int buf = (c.ring0 + ch) % c.NB;
+    BmWord *bw = c.bw_ring + (int64_t)buf * c.nwords;
+    const int64_t wbase = (int64_t)qa >> 6;
+    auto word_off = [&](int i) {  // candidate index of word i's first candidate
+        uint32_t wo = (uint32_t)(g0 + (i >> 2)) * kGroupCells;
+        for (int u = i & ~3; u < i; ++u) wo += (uint32_t)__popcll(s_bm[u]);
+        return wo;
+    };
+    for (int i = tid; i < nw; i += T) {
+        if (wbase + i >= c.nwords) continue;
+        BmWord v;
+        v.bm = s_bm[i];
+        v.wo = word_off(i);
+        v.pad = 0;
+        bw[wbase + i] = v;
+    }
+    // the records
+    const int cnt = min(s_cnt, cap);
+    CandHdr *hr = c.hdr_ring + (int64_t)buf * c.cstride;
+    CandVal *vr = c.val_ring + (int64_t)buf * c.cstride;
+    for (int i = tid; i < cnt; i += T) {
+        const int item = scr[i];
+        CandHdr hd;
+        CandVal v;
+        uint32_t q;
+        if (item >= cs) {  // S1
+            const int e = item;
+            q = c.pix[e];
+            const int4 lk = c.link[e];
+            const FlowCell fe = c.evf[e];
+            const FlowCell sn = lk.y >= 0 ? c.evf[lk.y] : c.fsnap[q];
+            hd.lin = q | (sn.L > 0 ? kCandSnapOk : 0u) | (fe.L > 0 ? kCandOneOk : 0u);
+            hd.e1 = e;
+            hd.t_snap = sn.t;
+            hd.t1 = fe.t;
+            v.L_snap = sn.L; v.Lc_snap = sn.Lc; v.Ls_snap = sn.Ls;
+            v.L1 = fe.L; v.Lc1 = fe.Lc; v.Ls1 = fe.Ls;
+            v.run_lo = lk.x;
+            v.run_hi = lk.x;
+            if (lk.z < ce) {  // more than one event at the cell in the chunk
+                hd.lin |= kCandMore;
+                const int e2 = lk.z;
+                const int4 lk2 = c.link[e2];
+                if (lk2.z < ce) {  // more than two: the run's last in-chunk position in P
+                    hd.lin |= kCandMore2;
+                    int a = lk2.x + 1, b = c.pend[q];  // P[a] = the third event < ce; ids ascend along the run
+                    while (a < b) {
+                        const int m = (a + b + 1) >> 1;
+                        if (c.P[m] < ce) a = m;
+                        else b = m - 1;
+                    }
+                    v.run_hi = a;
+                } else {  // exactly two: the second inline
+                    const FlowCell f2 = c.evf[e2];
+                    v.run_lo = (int32_t)((uint32_t)e2 | (f2.L > 0 ? 0x80000000u : 0u));
+                    v.run_hi = (int32_t)f2.t;
+                }
+            }
+        } else {  // S2 (an earlier event) or S3 (a call-start snapshot): untouched in the chunk
+            q = item >= 0 ? c.pix[item] : (uint32_t)~item;
+            const FlowCell sn = item >= 0 ? c.evf[item] : c.fsnap[q];
+            hd.lin = q | kCandSnapOk;
+            hd.e1 = INT_MAX;
+            hd.t_snap = sn.t;
+            hd.t1 = 0;
+            v.L_snap = sn.L; v.Lc_snap = sn.Lc; v.Ls_snap = sn.Ls;
+            v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
+            v.run_lo = 0;
+            v.run_hi = 0;
+        }
+        const int wi = (int)((q - qa) >> 6);
+        const uint32_t slot = word_off(wi) + (uint32_t)__popcll(s_bm[wi] & ((1ull << (q & 63)) - 1));
+        hr[slot] = hd;
+        vr[slot] = v;
+    }
+}
+
+// After a call's last k_cand: every cell's flow snapshot becomes its last
+// event's flow (k_chain advances them itself).
+__global__ void k_cand_commit(Ctx c) {
+    if (!c.cinfo[kCiFlag]) return;
+    const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (e >= c.n || c.link[e].z != INT_MAX) return;
+    const uint32_t q = c.pix[e];
+    FlowCell f = c.evf[e];
+    f.pad = 0;
+    c.fsnap[q] = f;
+    c.ftime[q] = f.L > 0 ? (int64_t)f.t : -1;
 }
 
 // Last event with id <= e over a candidate's in-chunk run P[lo..hi] (P[lo] <= e).
@@ -2659,9 +3001,13 @@ struct Work {
     FlowCell *evf = nullptr;
     int2 *dbg_tc = nullptr;
     uint32_t *ctmin = nullptr, *ctmax = nullptr;
+    uint32_t *cpmax = nullptr;                 // k_cand plan: prefix maximum of ctmax
+    int32_t *cbk = nullptr;                    // k_cand plan: first chunk reaching each chunk's kill window
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
     int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
+    int4 *slist = nullptr;                     // k_cand: the call-start snapshot list (<= kCandMaxList)
+    int *cinfo = nullptr;                      // k_cand: the call's plan (kCiWords)
     std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
     hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
     hipEvent_t ready = nullptr;                // two-phase calls: the fits and the imported flows are in place
@@ -2690,6 +3036,9 @@ struct farms_handle {
     CandHdr *hdr_ring = nullptr;
     CandVal *val_ring = nullptr;
     int64_t nwords = 0;
+    int cslices = 1, cgps = 0;   // k_cand: slices of the candidate groups, groups per slice
+    int32_t *cscr = nullptr;      // k_cand: candidate items per (chunk of a launch, slice)
+    int cand_set = -1;            // workspace set of the last call that built candidate lists
     int64_t chunk_base = 0, super_base = 0;  // pooling chunks / super-chunks enqueued since the last reset
     hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
     hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
@@ -2772,6 +3121,7 @@ void free_workspace(Work &w) {
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
+    dfree(w.cpmax); dfree(w.cbk);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -2803,7 +3153,8 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         (rc = dalloc(&w.link, cap)) || (rc = dalloc(&w.Q, cap)) || (rc = dalloc(&w.qe, cap)) || (rc = dalloc(&w.fdesc, cap)) ||
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
-        (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch))) {
+        (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch)) || (rc = dalloc(&w.cpmax, nch)) ||
+        (rc = dalloc(&w.cbk, nch))) {
         free_workspace(w);
         return rc;
     }
@@ -2901,6 +3252,7 @@ int reset_surfaces(farms_handle *h) {
     for (Work &w : h->ws) {
         HIPCHK(hipMemsetAsync(w.pcur, 0, sizeof(int32_t) * h->WH, h->stream));
         HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
+        HIPCHK(hipMemsetAsync(w.cinfo, 0, sizeof(int) * kCiWords, h->stream));
     }
     HIPCHK(hipStreamSynchronize(h->stream));
     if ((rc = clear_stats(h))) return rc;
@@ -2952,6 +3304,13 @@ pool_launcher pool_for(int K, int fr) {
 bool fit_quad_env() {
     const char *fq = getenv("FARMS_FIT_QUAD");
     return !(fq && fq[0] == '0');
+}
+// FARMS_CAND=events|chain: force the candidate build (A/B and test aid; every
+// choice gives the same bits); default: k_cand for time-local streams.
+int cand_force() {
+    const char *v = getenv("FARMS_CAND");
+    if (!v) return 0;
+    return v[0] == 'e' ? 1 : v[0] == 'c' ? 2 : 0;
 }
 int fit_mode_env() {
     const char *fu = getenv("FARMS_FIT_MODE");
@@ -3030,6 +3389,8 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.cells = SaeBuf{h->sae_head, h->sae_tail}; c.PT = w.PT; c.fsnap = h->fsnap; c.ftime = h->ftime;
     c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
     c.pcur = w.pcur; c.pend = w.pend;
+    c.cbk = w.cbk; c.slist = w.slist; c.cinfo = w.cinfo; c.cscr = h->cscr;
+    c.cgps = h->cgps; c.cslices = h->cslices;
     c.serial = h->prm.serial != 0;
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
@@ -3249,6 +3610,15 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     hipEvent_t t_pool0 = nullptr;  // the pooling sweep's start: the chain stream past the prep (phase 2: the fits)
     if (prof && phase != 1) { int rc = mark(h, sc, &t_pool0); if (rc) return rc; }
+    if (phase != 1 && n_pool_chunks > 0) {  // which candidate build takes the call (k_cand / k_chain)
+        hipLaunchKernelGGL(k_cand_plan_max, dim3(1), dim3(1024), 0, sc, w.ctmin, w.ctmax, n_pool_chunks, w.cpmax,
+                           w.cinfo);
+        hipLaunchKernelGGL(k_cand_plan_back, dim3(ceil_div(n_pool_chunks, 256)), dim3(256), 0, sc, w.ctmin, w.cpmax,
+                           n_pool_chunks, w.cbk, w.cinfo);
+        hipLaunchKernelGGL(k_cand_list, dim3(ceil_div(h->WH, 256)), dim3(256), 0, sc, c, w.slist);
+        hipLaunchKernelGGL(k_cand_flag, dim3(1), dim3(1), 0, sc, w.cinfo, cand_force());
+        h->cand_set = (int)(&w - h->ws);
+    }
     int fit_enqueued = 0, fit_waited = -1;
     if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
         while (fit_enqueued < n_fit_chunks) {
@@ -3292,8 +3662,13 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
-        for (int a = ch0; a < ch1; a += 64)  // <= 64 chunks per launch (their spans in one VGPR)
-            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, std::min(a + 64, ch1));
+        for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (their spans in one VGPR)
+            // one of the two builds the lists (cinfo[kCiFlag]); the other leaves at once
+            const int b = std::min(a + 64, ch1);
+            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
+            hipLaunchKernelGGL(k_cand, dim3((b - a) * h->cslices), dim3(kCandThreads),
+                               sizeof(uint64_t) * 4 * (size_t)h->cgps, sc, c, a, b);
+        }
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
@@ -3323,7 +3698,10 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     }
     h->super_base += n_super;
     h->chunk_base += n_pool_chunks;
-    if (n_super > 0) HIPCHK(hipEventRecord(h->chain_end, sc));
+    if (n_super > 0) {  // the snapshots advance to the call's last events (k_cand calls)
+        hipLaunchKernelGGL(k_cand_commit, dim3(ceil_div(n, 256)), dim3(256), 0, sc, c);
+        HIPCHK(hipEventRecord(h->chain_end, sc));
+    }
     HIPCHK(hipGetLastError());
     if (phase != 2) {
         h->acc.n_events += n;
@@ -3350,13 +3728,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             HIPCHK(hipEventRecord(w.fend, s));
             HIPCHK(hipStreamWaitEvent(sp, w.fend, 0));
         }
+        HIPCHK(hipStreamWaitEvent(sp, h->chain_end, 0));  // k_cand_commit reads the set's links and flows
         HIPCHK(hipEventRecord(w.done, sp));
         w.busy = true;
         return FARMS_OK;
     }
     // join: stream F waits for the last chain step and the last pooling launch
     if (n_super > 0) {
-        HIPCHK(hipStreamWaitEvent(s, ev_cand(n_super - 1), 0));
+        HIPCHK(hipStreamWaitEvent(s, h->chain_end, 0));
         HIPCHK(hipStreamWaitEvent(s, ev_pool(n_super - 1), 0));
     }
     if (h->counting) {  // k_stats ran on P after the last pooling launch
@@ -3464,6 +3843,11 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->nwords = (h->WH + 63) / 64;
     h->nblk = (int)((h->WH + kGroupCells - 1) / kGroupCells);
     h->cstride = (int64_t)h->nblk * kGroupCells;
+    // k_cand slices: at most kCandSliceGroups groups each (FARMS_CAND_SLICES, A/B aid: more of them)
+    h->cslices = (h->nblk + kCandSliceGroups - 1) / kCandSliceGroups;
+    if (const char *v = getenv("FARMS_CAND_SLICES")) h->cslices = std::max(h->cslices, std::min(atoi(v), h->nblk));
+    h->cgps = (h->nblk + h->cslices - 1) / h->cslices;
+    h->cslices = (h->nblk + h->cgps - 1) / h->cgps;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     {
@@ -3528,7 +3912,11 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 2)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     for (Work &w : h->ws)
-        if ((rc = dalloc(&w.pcur, h->WH)) || (rc = dalloc(&w.pend, h->WH))) return bail(rc);
+        if ((rc = dalloc(&w.pcur, h->WH)) || (rc = dalloc(&w.pend, h->WH)) ||
+            (rc = dalloc(&w.slist, std::min<int64_t>(h->WH, kCandMaxList))) || (rc = dalloc(&w.cinfo, kCiWords)))
+            return bail(rc);
+    if ((rc = dalloc(&h->cscr, (size_t)std::min(h->pool_batch, 64) * h->cslices * h->cgps * kGroupCells)))
+        return bail(rc);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
     return FARMS_OK;
@@ -3543,7 +3931,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     dfree(h->sae_head); dfree(h->sae_tail); dfree(h->ftime); dfree(h->fsnap);
     for (Work &w : h->ws) {
         free_workspace(w);
-        dfree(w.pcur); dfree(w.pend);
+        dfree(w.pcur); dfree(w.pend); dfree(w.slist); dfree(w.cinfo);
         for (auto &ev : w.sync_ev) (void)hipEventDestroy(ev);
         if (w.done) (void)hipEventDestroy(w.done);
         if (w.ready) (void)hipEventDestroy(w.ready);
@@ -3554,7 +3942,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     for (auto &ev : h->up_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (h->chain_end) (void)hipEventDestroy(h->chain_end);
-    dfree(h->bw_ring);
+    dfree(h->bw_ring); dfree(h->cscr);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &b : h->brk) {
         h->ev_free.push_back(b.a);
@@ -3612,9 +4000,17 @@ extern "C" int farms_kernel_info(const farms_handle *h, char *buf, int32_t len) 
     if (!fast) fit = "k_fit_wave";
     else if (!quad) fit = "k_fit<" + fr + ">";
     else fit = "k_fit_quad<" + fr + ">";
+    // the candidate build the last pooling call took (decided on the device per call)
+    std::string cand;
+    if (h->cand_set >= 0) {
+        int flag = 0;
+        HIPCHK(hipStreamSynchronize(h->s_chain));
+        HIPCHK(hipMemcpy(&flag, h->ws[h->cand_set].cinfo + kCiFlag, sizeof(int), hipMemcpyDeviceToHost));
+        cand = flag ? "k_cand" : "k_chain";
+    }
     const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(fast && quad ? mode : -1) +
                            ", \"pool\": \"k_pool<" + std::to_string(h->K) + ">\", \"pool_cap\": " +
-                           (pool_w7(h->fr) ? "7" : "6") + "}";
+                           (pool_w7(h->fr) ? "7" : "6") + ", \"cand_last\": \"" + cand + "\"}";
     std::snprintf(buf, (size_t)len, "%s", js.c_str());
     return FARMS_OK;
 }

@@ -205,10 +205,11 @@ int farms_serial_first(farms_handle *h, int32_t x, int32_t y, uint32_t t_abs);
 int farms_num_scales(const farms_handle *h);
 
 /* The kernels the handle's next call runs (its filter and scales, and the
- * FARMS_FIT_* / FARMS_POOL_* tuning knobs as they are now), as a JSON object
- * in buf (NUL-terminated, truncated to len): {"fit": "k_fit_box<2>",
- * "fit_mode": 3, "fit_solve": "", "pool": "k_pool<11>", "pool_group": 1,
- * "pool_cap": 7}.  Not in the reference (measurement aid for bench.py). */
+ * FARMS_FIT_* / FARMS_POOL_* tuning knobs as they are now), and the candidate
+ * build the last pooling call took (decided on the device per call; waits for
+ * it), as a JSON object in buf (NUL-terminated, truncated to len):
+ * {"fit": "k_fit_quad<2>", "fit_mode": 1, "pool": "k_pool<11>", "pool_cap": 7,
+ * "cand_last": "k_cand"}.  Not in the reference (measurement aid for bench.py). */
 int farms_kernel_info(const farms_handle *h, char *buf, int32_t len);
 
 /* Thread-local message for the last non-OK status. */

@@ -483,3 +483,59 @@ def test_serial_first_only_on_a_fresh_handle():
         assert lt[3 * 32 + 4] == 0 and lt[1 * 32 + 1] == 5  # the event's own (relative) stamp 0 now
         fm.reset()
         fm.serial_first(3, 4, 777)
+
+
+def _process(x, y, t, p, H, W, fs, splits=None, serial_first=None, **kw):
+    with farms.FlowManager(H, W, fs, 5, serial=serial_first is not None, **kw) as fm:
+        if serial_first is not None:
+            fm.serial_first(*serial_first)
+        if splits is None:
+            g = fm.process(x, y, t, p)
+            g = {c: getattr(g, c) for c in farms.COLUMNS}
+        else:
+            parts = [fm.process(x[a:b], y[a:b], t[a:b], p[a:b]) for a, b in splits]
+            g = {c: np.concatenate([getattr(q, c) for q in parts]) for c in farms.COLUMNS}
+        return g, fm.kernel_info()["cand_last"]
+
+
+def test_candidate_builds_are_bitwise_identical(monkeypatch):
+    """The pooling candidate lists come from k_cand (event-driven, chunks
+    independent) on time-local streams and from k_chain (the per-cell chain)
+    otherwise; FARMS_CAND forces either.  Both give the same bits on every
+    stream shape: time-ordered (C3, with many small pooling chunks too, and C4's
+    fs 7), split across calls, serial mode, and out-of-order stamps."""
+    ev3 = farms.synth_config(3, 200_000)
+    x3, y3, t3, p3 = ev3.relative()
+    ev2 = farms.synth_config(2, 120_000)
+    x2, y2, t2, p2 = ev2.relative()
+    rng = np.random.default_rng(11)
+    tu = t2.astype(np.int64)
+    swap = rng.random(tu.shape[0]) < 0.05
+    tu[swap] = rng.integers(0, int(tu.max()) + 1, swap.sum())
+    tu = tu.astype(np.uint32)
+    ev4 = farms.synth_config(4, 150_000)
+    x4, y4, t4, p4 = ev4.relative()
+    first, xs, ys, ts, ps = serial_inputs(farms.synth_config(1, 60_001))
+    cases = [
+        ("c3", (x3, y3, t3, p3, 720, 1280, 5), {}, "k_cand"),
+        ("c3_small_chunks", (x3, y3, t3, p3, 720, 1280, 5), {"pool_chunk": 1024, "pool_batch": 16}, "k_cand"),
+        ("c4", (x4, y4, t4, p4, 720, 1280, 7), {}, "k_cand"),
+        ("c2_split", (x2, y2, t2, p2, 320, 320, 5), {"splits": [(0, 1), (1, 40_000), (40_000, 40_001),
+                                                              (40_001, 120_000)]}, "k_cand"),
+        ("c1_serial", (xs, ys, ts, ps, 128, 128, 3), {"serial_first": first, "splits": [(0, 7), (7, 30_000),
+                                                                                      (30_000, len(xs))]}, "k_cand"),
+        # (235 chunks: the random stamps reach back further than kCandMaxBack)
+        ("c2_unsorted", (x2, y2, tu, p2, 320, 320, 5), {"pool_chunk": 512}, "k_chain"),
+    ]
+    for name, args, kw, default in cases:
+        outs = {}
+        for mode in ("", "events", "chain"):
+            if mode:
+                monkeypatch.setenv("FARMS_CAND", mode)
+            else:
+                monkeypatch.delenv("FARMS_CAND", raising=False)
+            outs[mode], used = _process(*args, **kw)
+            want = {"": default, "events": "k_cand", "chain": "k_chain"}[mode]
+            assert used == want, (name, mode, used)
+        for mode in ("events", "chain"):
+            assert bitwise_equal(outs[""], outs[mode]), (name, mode, compare(outs[""], outs[mode]))

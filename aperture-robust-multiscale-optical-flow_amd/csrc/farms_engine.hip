@@ -32,6 +32,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <climits>
 #include <chrono>
@@ -225,8 +226,10 @@ struct Ctx {
     const int32_t *cbk;
     const int4 *slist;
     int *cinfo;
-    int32_t *cscr;
-    int cgps, cslices;     // candidate groups per slice, slices
+    int32_t *cscr;         // k_cand scratch: per chunk of a launch, WH item slots (a band's at its first cell)
+    const int32_t *bstart; // k_cand: per pooling chunk, the work-order start of each column band (nbands + 1)
+    int nbands, bandc;     // column bands, columns per band (bandc * H: whole candidate groups)
+    int tilesH, tshift;    // work-order tiles per column, log2 of the tile edge
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
     // with its pixel's lastEventTime still holding link.w, the stamp before it
     // (written only after pooling, :790)
@@ -1849,20 +1852,17 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
 constexpr int kGroupCells = 256;
 
 // The call's candidate-build plan (Ctx::cinfo, per workspace set):
-//   kCiFlag     1: k_cand builds the candidate lists, 0: k_chain does
+//   kCiFlag     (unused)
 //   kCiMaxBack  largest chunk distance back to cbk (k_cand_plan_back)
 //   kCiCount    call-start snapshot list length (k_cand_list)
 //   kCiLMin/Max stamp range of that list
 //   kCiTMin/Max stamp range of the call's events
 enum { kCiFlag = 0, kCiMaxBack, kCiCount, kCiLMin, kCiLMax, kCiTMin, kCiTMax, kCiWords };
 // k_cand takes a call when every chunk's kill window reaches back at most this
-// many chunks (a time-ordered stream: 2-3) and the call-start snapshot list
-// inside the call's stamp span is at most kCandMaxList cells; other streams
-// (out-of-order stamps) keep k_chain, whose cost is independent of the order.
+// many chunks (a time-ordered stream: 2-3); other streams (out-of-order stamps)
+// keep k_chain, whose cost is independent of the order.  The host reads the
+// reach after the call's prep (k_cand_plan_back) and launches one of the two.
 constexpr int kCandMaxBack = 64;
-constexpr int kCandMaxList = 1 << 18;
-constexpr int kCandThreads = 512;
-constexpr int kCandSliceGroups = 1024;  // candidate groups per k_cand slice at most (32 KB of LDS bitmap)
 
 
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling
@@ -1907,7 +1907,6 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
     const int lane = threadIdx.x & 63;
     const int64_t g = (int64_t)blockIdx.x;
     if (g >= c.nblk) return;
-    if (c.cinfo[kCiFlag]) return;  // k_cand builds this call's candidates
     const int n = c.n, C2 = c.C2;
     const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
     const uint64_t lt = (1ull << lane) - 1;
@@ -2164,65 +2163,80 @@ __global__ void k_cand_list(Ctx c, int4 *list) {
     base = __shfl(base, leader, 64);
     if (keep) {
         const int i = base + (int)__popcll(bal & ((1ull << lane) - 1));
-        if (i < kCandMaxList) list[i] = ent;  // a longer list hands the call to k_chain
+        list[i] = ent;
         atomicMin(reinterpret_cast<unsigned int *>(&info[kCiLMin]), (unsigned int)ent.y);
         atomicMax(reinterpret_cast<unsigned int *>(&info[kCiLMax]), (unsigned int)ent.y);
     }
 }
 
-// force: 0 by the stream, 1 k_cand (unless the list overflowed), 2 k_chain
-// (FARMS_CAND, A/B and test aid).
-__global__ void k_cand_flag(int *info, int force) {
-    const bool fits = info[kCiCount] <= kCandMaxList;  // the list holds every call-start snapshot needed
-    const bool local = info[kCiMaxBack] <= kCandMaxBack;
-    info[kCiFlag] = fits && force != 2 && (force == 1 || local) ? 1 : 0;
+// Work-order bounds of the column bands (k_cand): the work order Q is sorted by
+// (pooling chunk, 8x8 tile), tiles x-major, so the events of chunk ch in the
+// band of columns [b * bandc, (b + 1) * bandc) are the positions
+// [bstart[ch * (nbands + 1) + b], bstart[ch * (nbands + 1) + b + 1]).
+__global__ void k_band_starts(Ctx c, const uint32_t *wkey_sorted, int tile_bits, int32_t *bstart) {
+    const int w = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (w >= c.n) return;
+    const int ch = w / c.C2, cs = ch * c.C2, ce = min(cs + c.C2, c.n);
+    const uint32_t tmask = (1u << tile_bits) - 1;
+    const int tpb = c.bandc >> c.tshift;  // tile columns per band
+    auto band = [&](int i) { return (int)((wkey_sorted[i] & tmask) / (uint32_t)c.tilesH) / tpb; };
+    const int bw = band(w), pb = w > cs ? band(w - 1) : -1;
+    int32_t *bs = bstart + (int64_t)ch * (c.nbands + 1);
+    for (int b = pb + 1; b <= bw; ++b) bs[b] = w;
+    if (w == ce - 1)
+        for (int b = bw + 1; b <= c.nbands; ++b) bs[b] = ce;
 }
 
-// One workgroup per (pooling chunk, slice of cgps candidate groups) of chunks
-// [ch0, ch1).
-__global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) {
-    if (!c.cinfo[kCiFlag]) return;  // k_chain builds this call's candidates
-    extern __shared__ uint64_t s_bm[];  // the slice's bitmap words
-    __shared__ int s_cnt;
-    const int lb = work_block();  // XCD-contiguous: the slices of a chunk share an L2
-    const int ch = ch0 + lb / c.cslices, sl = lb % c.cslices;
+// One wavefront (= one workgroup: it slots in as the pooling waves free theirs)
+// per (pooling chunk, band of columns) of chunks [ch0, ch1).  A band's cells
+// [b * bandc * H, ...) start on a candidate-group boundary (bandc * H is a
+// multiple of 256), so its bitmap words and their group-local offsets are its
+// own; its events of any chunk are one range of the work order (bstart).
+__global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
+    extern __shared__ uint64_t s_bm[];  // the band's bitmap words
+    const int lb = work_block();  // XCD-contiguous: neighbouring bands share an L2
+    const int ch = ch0 + lb / c.nbands, bd = lb % c.nbands;
     if (ch >= ch1) return;
-    const int tid = (int)threadIdx.x, T = (int)blockDim.x, lane = tid & 63;
-    const int g0 = sl * c.cgps, g1 = min(g0 + c.cgps, c.nblk);
-    if (g0 >= g1) return;
-    const uint32_t qa = (uint32_t)g0 * kGroupCells, qb = (uint32_t)min((int64_t)g1 * kGroupCells, c.WH);
-    const int nw = (g1 - g0) * 4;
-    for (int i = tid; i < nw; i += T) s_bm[i] = 0;
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
+    const int lane = (int)threadIdx.x;
+    const int H = c.H;
+    const uint32_t qa = (uint32_t)bd * (uint32_t)c.bandc * (uint32_t)H;
+    const uint32_t qb = (uint32_t)min((int64_t)qa + (int64_t)c.bandc * H, c.WH);
+    const int nw = (int)((qb - qa + 63) >> 6);
+    const int g0 = (int)(qa / kGroupCells);
+    for (int i = lane; i < nw; i += 64) s_bm[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     const int n = c.n, C2 = c.C2;
     const int cs = ch * C2, ce = min(cs + C2, n);
     const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
-    const int cap = c.cgps * kGroupCells;
-    int32_t *scr = c.cscr + ((int64_t)(ch - ch0) * c.cslices + sl) * (int64_t)cap;
+    const int cap = (int)(qb - qa);
+    int32_t *scr = c.cscr + (int64_t)(ch - ch0) * c.WH + qa;  // this band's item slots in the chunk's scratch
     const uint64_t lt = (1ull << lane) - 1;
-    // mark q, keep the item (wave-aggregated slot claim)
+    const int OFF = c.X0 * H;
+    int cnt = 0;  // (wave-uniform)
     auto push = [&](bool keep, uint32_t q, int item) {
         const uint64_t bal = __ballot(keep);
-        if (!bal) return;
-        const int leader = __ffsll((unsigned long long)bal) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&s_cnt, (int)__popcll(bal));
-        base = __shfl(base, leader, 64);
         if (keep) {
             atomicOr((unsigned long long *)&s_bm[(q - qa) >> 6], 1ull << (q & 63));
-            const int i = base + (int)__popcll(bal & lt);
+            const int i = cnt + (int)__popcll(bal & lt);
             if (i < cap) scr[i] = item;  // (a cell is an item at most once: i < cap always)
         }
+        cnt += (int)__popcll(bal);
     };
+    const int32_t *bsr = c.bstart + (int64_t)bd;
+    const int64_t bstride = c.nbands + 1;
     // S1: first events of the chunk at their cells
-    for (int e0 = cs; e0 < ce; e0 += T) {
-        const int e = e0 + tid;
-        bool keep = false;
-        uint32_t q = 0;
-        if (e < ce) {
-            q = c.pix[e];
-            if (q >= qa && q < qb) {
+    {
+        const int w0 = bsr[ch * bstride], w1 = bsr[ch * bstride + 1];
+        for (int wb = w0; wb < w1; wb += 64) {
+            const int w = wb + lane;
+            bool keep = false;
+            uint32_t q = 0;
+            int e = 0;
+            if (w < w1) {
+                const int4 fd = c.fdesc[w];  // {event, x, y, t}
+                e = fd.x;
+                q = (uint32_t)(fd.y * H + fd.z - OFF);
                 const int4 lk = c.link[e];
                 if (lk.y < cs) {
                     if (lk.z < ce) keep = true;
@@ -2234,23 +2248,26 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
                     }
                 }
             }
+            push(keep, q, e);
         }
-        push(keep, q, e);
     }
     // S2: the last events before the chunk at untouched cells, from the chunks
     // whose stamps reach the kill window
     for (int cp = c.cbk[ch]; cp < ch; ++cp) {
         if (!((int64_t)c.ctmax[cp] > lo && (int64_t)c.ctmin[cp] < hi)) continue;
-        const int a = cp * C2, b = min(a + C2, n);
-        for (int e0 = a; e0 < b; e0 += T) {
-            const int e = e0 + tid;
+        const int w0 = bsr[cp * bstride], w1 = bsr[cp * bstride + 1];
+        for (int wb = w0; wb < w1; wb += 64) {
+            const int w = wb + lane;
             bool keep = false;
             uint32_t q = 0;
-            if (e < b) {
-                const int64_t te = (int64_t)c.t[e];
+            int e = 0;
+            if (w < w1) {
+                const int4 fd = c.fdesc[w];
+                const int64_t te = (int64_t)(uint32_t)fd.w;
+                e = fd.x;
                 if (te > lo && te < hi) {
-                    q = c.pix[e];
-                    if (q >= qa && q < qb && c.link[e].z >= ce) keep = c.evf[e].L > 0;
+                    q = (uint32_t)(fd.y * H + fd.z - OFF);
+                    if (c.link[e].z >= ce) keep = c.evf[e].L > 0;
                 }
             }
             push(keep, q, e);
@@ -2258,13 +2275,13 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
     }
     // S3: call-start snapshots of cells the call has not touched before ce
     {
-        const int cnt = c.cinfo[kCiCount];
-        if (cnt > 0 && (int64_t)(uint32_t)c.cinfo[kCiLMax] > lo && (int64_t)(uint32_t)c.cinfo[kCiLMin] < hi) {
-            for (int i0 = 0; i0 < cnt; i0 += T) {
-                const int i = i0 + tid;
+        const int ns = c.cinfo[kCiCount];
+        if (ns > 0 && (int64_t)(uint32_t)c.cinfo[kCiLMax] > lo && (int64_t)(uint32_t)c.cinfo[kCiLMin] < hi) {
+            for (int i0 = 0; i0 < ns; i0 += 64) {
+                const int i = i0 + lane;
                 bool keep = false;
                 uint32_t q = 0;
-                if (i < cnt) {
+                if (i < ns) {
                     const int4 en = c.slist[i];
                     q = (uint32_t)en.x;
                     const int64_t ft = (int64_t)(uint32_t)en.y;
@@ -2274,7 +2291,8 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
             }
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     // bitmap words with the group-local offset of their first candidate
     const int buf = (c.ring0 + ch) % c.NB;
     BmWord *bw = c.bw_ring + (int64_t)buf * c.nwords;
@@ -2284,8 +2302,7 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
         for (int u = i & ~3; u < i; ++u) wo += (uint32_t)__popcll(s_bm[u]);
         return wo;
     };
-    for (int i = tid; i < nw; i += T) {
-        if (wbase + i >= c.nwords) continue;
+    for (int i = lane; i < nw; i += 64) {
         BmWord v;
         v.bm = s_bm[i];
         v.wo = word_off(i);
@@ -2293,10 +2310,10 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
         bw[wbase + i] = v;
     }
     // the records
-    const int cnt = min(s_cnt, cap);
+    cnt = min(cnt, cap);
     CandHdr *hr = c.hdr_ring + (int64_t)buf * c.cstride;
     CandVal *vr = c.val_ring + (int64_t)buf * c.cstride;
-    for (int i = tid; i < cnt; i += T) {
+    for (int i = lane; i < cnt; i += 64) {
         const int item = scr[i];
         CandHdr hd;
         CandVal v;
@@ -2356,7 +2373,6 @@ __global__ __launch_bounds__(kCandThreads) void k_cand(Ctx c, int ch0, int ch1) 
 // After a call's last k_cand: every cell's flow snapshot becomes its last
 // event's flow (k_chain advances them itself).
 __global__ void k_cand_commit(Ctx c) {
-    if (!c.cinfo[kCiFlag]) return;
     const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (e >= c.n || c.link[e].z != INT_MAX) return;
     const uint32_t q = c.pix[e];
@@ -3003,11 +3019,13 @@ struct Work {
     uint32_t *ctmin = nullptr, *ctmax = nullptr;
     uint32_t *cpmax = nullptr;                 // k_cand plan: prefix maximum of ctmax
     int32_t *cbk = nullptr;                    // k_cand plan: first chunk reaching each chunk's kill window
+    int32_t *bstart = nullptr;                 // k_cand: per chunk, the work-order start of each column band
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
     int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
     int4 *slist = nullptr;                     // k_cand: the call-start snapshot list (<= kCandMaxList)
     int *cinfo = nullptr;                      // k_cand: the call's plan (kCiWords)
+    hipEvent_t plan_ev = nullptr;              // the plan's reach (kCiMaxBack) is in the handle's pinned word
     std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
     hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
     hipEvent_t ready = nullptr;                // two-phase calls: the fits and the imported flows are in place
@@ -3036,9 +3054,11 @@ struct farms_handle {
     CandHdr *hdr_ring = nullptr;
     CandVal *val_ring = nullptr;
     int64_t nwords = 0;
-    int cslices = 1, cgps = 0;   // k_cand: slices of the candidate groups, groups per slice
+    int nbands = 1, bandc = 0;   // k_cand: column bands, columns per band
+    bool cand_ok = true;          // the bands fit k_cand's LDS bitmap (else every call takes k_chain)
     int32_t *cscr = nullptr;      // k_cand: candidate items per (chunk of a launch, slice)
-    int cand_set = -1;            // workspace set of the last call that built candidate lists
+    int cand_last = -1;           // the last pooling call's candidate build: 1 k_cand, 0 k_chain
+    int *plan_pin = nullptr;      // pinned: kCiMaxBack of each workspace set's last prep
     int64_t chunk_base = 0, super_base = 0;  // pooling chunks / super-chunks enqueued since the last reset
     hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
     hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
@@ -3121,7 +3141,7 @@ void free_workspace(Work &w) {
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
-    dfree(w.cpmax); dfree(w.cbk);
+    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -3154,7 +3174,7 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
         (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch)) || (rc = dalloc(&w.cpmax, nch)) ||
-        (rc = dalloc(&w.cbk, nch))) {
+        (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1)))) {
         free_workspace(w);
         return rc;
     }
@@ -3390,7 +3410,8 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
     c.pcur = w.pcur; c.pend = w.pend;
     c.cbk = w.cbk; c.slist = w.slist; c.cinfo = w.cinfo; c.cscr = h->cscr;
-    c.cgps = h->cgps; c.cslices = h->cslices;
+    c.bstart = w.bstart; c.nbands = h->nbands; c.bandc = h->bandc;
+    c.tshift = h->tile_shift; c.tilesH = (h->H + (1 << h->tile_shift) - 1) >> h->tile_shift;
     c.serial = h->prm.serial != 0;
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
@@ -3429,7 +3450,7 @@ int claim_set(farms_handle *h, Work &w, int n, hipEvent_t *t_start) {
         int rc = mark(h, s, t_start);
         if (rc) return rc;
     }
-    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
+    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 3 * (size_t)n_super);
 }
 
 // The prep of a call on set w (stream F): validate, pixel ids, sort by pixel,
@@ -3471,7 +3492,16 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
                                                   h->tile_bits + cb, s));
     }
     hipLaunchKernelGGL(k_fit_desc, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
+    hipLaunchKernelGGL(k_band_starts, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.wkey_sorted, h->tile_bits, w.bstart);
     hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
+    if (n_pool_chunks > 0) {  // the candidate build's plan: how far back each chunk's kill window reaches
+        hipLaunchKernelGGL(k_cand_plan_max, dim3(1), dim3(1024), 0, s, w.ctmin, w.ctmax, n_pool_chunks, w.cpmax,
+                           w.cinfo);
+        hipLaunchKernelGGL(k_cand_plan_back, dim3(ceil_div(n_pool_chunks, 256)), dim3(256), 0, s, w.ctmin, w.cpmax,
+                           n_pool_chunks, w.cbk, w.cinfo);
+        HIPCHK(hipMemcpyAsync(h->plan_pin + (&w - h->ws), w.cinfo + kCiMaxBack, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(w.plan_ev, s));
+    }
     HIPCHK(hipEventRecord(ev_prep, s));
     if (t_prep) {
         if ((rc = mark(h, s, t_prep))) return rc;
@@ -3522,11 +3552,15 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (rc) return rc;
     }
     // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
-    // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
+    // S: cand[S] (its candidate lists built), pool[S] (its pooling done),
+    // flow[S] (its local flows final: k_flow on F after its fits)
     hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
     auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
-    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
-    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
+    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 3 * S]; };
+    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 3 * S]; };
+    auto ev_flow = [&](int S) { return w.sync_ev[3 + n_fit_chunks + 3 * S]; };
+    auto super_end = [&](int S) { return (int)std::min<int64_t>((int64_t)(S + 1) * B * h->pool_chunk, n); };
+    int flow_next = 0;  // phase 0: the next super-chunk whose k_flow is not enqueued
     if (phase == 2) ev_prep = w.ready;  // prepared by phase 1: its fits and the imported flows are in place
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
@@ -3590,6 +3624,15 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
+        // the local flows of every super-chunk whose fits are now all enqueued,
+        // on F right behind them (one-wave blocks: they take slots as the
+        // pooling waves free them), so that the chain stream only waits for them
+        while (phase == 0 && flow_next < n_super && (f == n_fit_chunks - 1 || c1 >= super_end(flow_next))) {
+            const int q0 = flow_next * B * h->pool_chunk, q1 = super_end(flow_next);
+            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 64)), dim3(64), 0, s, c, q0, q1);
+            HIPCHK(hipEventRecord(ev_flow(flow_next), s));
+            ++flow_next;
+        }
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
             FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
             fin.blocks = ceil_div(n - c0, 64);
@@ -3610,16 +3653,25 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     hipEvent_t t_pool0 = nullptr;  // the pooling sweep's start: the chain stream past the prep (phase 2: the fits)
     if (prof && phase != 1) { int rc = mark(h, sc, &t_pool0); if (rc) return rc; }
-    if (phase != 1 && n_pool_chunks > 0) {  // which candidate build takes the call (k_cand / k_chain)
-        hipLaunchKernelGGL(k_cand_plan_max, dim3(1), dim3(1024), 0, sc, w.ctmin, w.ctmax, n_pool_chunks, w.cpmax,
-                           w.cinfo);
-        hipLaunchKernelGGL(k_cand_plan_back, dim3(ceil_div(n_pool_chunks, 256)), dim3(256), 0, sc, w.ctmin, w.cpmax,
-                           n_pool_chunks, w.cbk, w.cinfo);
-        hipLaunchKernelGGL(k_cand_list, dim3(ceil_div(h->WH, 256)), dim3(256), 0, sc, c, w.slist);
-        hipLaunchKernelGGL(k_cand_flag, dim3(1), dim3(1), 0, sc, w.cinfo, cand_force());
-        h->cand_set = (int)(&w - h->ws);
-    }
-    int fit_enqueued = 0, fit_waited = -1;
+    // the candidate build of the call (k_cand / k_chain), decided on the host
+    // from the plan once the first super-chunk's fits are enqueued
+    int use_cand = -1;
+    auto decide_cand = [&]() -> int {
+        const int force = cand_force();
+        if (!h->cand_ok) {
+            use_cand = 0;
+        } else if (force) {
+            use_cand = force == 1;
+        } else {
+            HIPCHK(hipEventSynchronize(w.plan_ev));
+            use_cand = h->plan_pin[&w - h->ws] <= kCandMaxBack;
+        }
+        h->cand_last = use_cand;
+        if (use_cand)  // the call-start snapshot list (after the previous call's k_cand_commit on C)
+            hipLaunchKernelGGL(k_cand_list, dim3(ceil_div(h->WH, 256)), dim3(256), 0, sc, c, w.slist);
+        return FARMS_OK;
+    };
+    int fit_enqueued = 0;
     if (phase == 1) {  // the whole fit sweep and the local flows, then back to the caller
         while (fit_enqueued < n_fit_chunks) {
             int rc = enqueue_fit(fit_enqueued++);
@@ -3639,7 +3691,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         h->acc.fit_launches += fit_launches;
         return FARMS_OK;
     }
-    if (phase == 2) { fit_enqueued = n_fit_chunks; fit_waited = n_fit_chunks - 1; }  // fits done (phase 1)
+    if (phase == 2) fit_enqueued = n_fit_chunks;  // fits done (phase 1)
     const int64_t sb = h->super_base;  // global number of this call's first super-chunk
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
@@ -3653,21 +3705,17 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
         if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
-        {  // the chain reads the local flows of every event of the super-chunk
-            const int f = (int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk);
-            const int fl = std::min(f, n_fit_chunks - 1);
-            if (fl > fit_waited) { HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0)); fit_waited = fl; }
-        }
-        if (phase != 2) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
-            const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
-            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
-        }
-        for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (their spans in one VGPR)
-            // one of the two builds the lists (cinfo[kCiFlag]); the other leaves at once
+        // the chain reads the local flows of every event of the super-chunk
+        // (phase 2: final since phase 1)
+        if (phase == 0) HIPCHK(hipStreamWaitEvent(sc, ev_flow(S), 0));
+        if (use_cand < 0) { int rc = decide_cand(); if (rc) return rc; }
+        for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (k_chain: their spans in one VGPR)
             const int b = std::min(a + 64, ch1);
-            hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
-            hipLaunchKernelGGL(k_cand, dim3((b - a) * h->cslices), dim3(kCandThreads),
-                               sizeof(uint64_t) * 4 * (size_t)h->cgps, sc, c, a, b);
+            if (use_cand)
+                hipLaunchKernelGGL(k_cand, dim3((b - a) * h->nbands), dim3(64),
+                               sizeof(uint64_t) * (size_t)ceil_div((int64_t)h->bandc * h->H, 64), sc, c, a, b);
+            else
+                hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
         }
         {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
@@ -3698,8 +3746,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     }
     h->super_base += n_super;
     h->chunk_base += n_pool_chunks;
-    if (n_super > 0) {  // the snapshots advance to the call's last events (k_cand calls)
-        hipLaunchKernelGGL(k_cand_commit, dim3(ceil_div(n, 256)), dim3(256), 0, sc, c);
+    if (n_super > 0) {  // k_cand calls: the snapshots advance to the call's last events
+        if (use_cand == 1) hipLaunchKernelGGL(k_cand_commit, dim3(ceil_div(n, 256)), dim3(256), 0, sc, c);
         HIPCHK(hipEventRecord(h->chain_end, sc));
     }
     HIPCHK(hipGetLastError());
@@ -3843,11 +3891,6 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->nwords = (h->WH + 63) / 64;
     h->nblk = (int)((h->WH + kGroupCells - 1) / kGroupCells);
     h->cstride = (int64_t)h->nblk * kGroupCells;
-    // k_cand slices: at most kCandSliceGroups groups each (FARMS_CAND_SLICES, A/B aid: more of them)
-    h->cslices = (h->nblk + kCandSliceGroups - 1) / kCandSliceGroups;
-    if (const char *v = getenv("FARMS_CAND_SLICES")) h->cslices = std::max(h->cslices, std::min(atoi(v), h->nblk));
-    h->cgps = (h->nblk + h->cslices - 1) / h->cslices;
-    h->cslices = (h->nblk + h->cgps - 1) / h->cgps;
     // fit chunks are whole pooling chunks (Q is grouped by pooling chunk)
     h->fit_chunk = (int)(((int64_t)h->fit_chunk + h->pool_chunk - 1) / h->pool_chunk * h->pool_chunk);
     {
@@ -3856,6 +3899,12 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         const int tm = (1 << h->tile_shift) - 1;
         const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);
         while ((int64_t(1) << h->tile_bits) < tiles) ++h->tile_bits;
+        // k_cand's column bands: whole candidate groups (bandc * H a multiple of
+        // 256) and whole work-order tile columns
+        const int gq = 256 / std::gcd(h->H, 256), tw = 1 << h->tile_shift;
+        h->bandc = gq / std::gcd(gq, tw) * tw;
+        h->nbands = (h->WR + h->bandc - 1) / h->bandc;
+        h->cand_ok = (int64_t)h->bandc * h->H <= (int64_t)64 * 4096;  // LDS bitmap of a band <= 32 KB
     }
     int rc = FARMS_OK;
     auto bail = [&](int code) { farms_destroy(h); return code; };
@@ -3900,6 +3949,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
             evs.push_back(&w.done);
             evs.push_back(&w.ready);
             evs.push_back(&w.fend);
+            evs.push_back(&w.plan_ev);
         }
         for (hipEvent_t *ev : evs)
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
@@ -3913,10 +3963,11 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         return bail(rc);
     for (Work &w : h->ws)
         if ((rc = dalloc(&w.pcur, h->WH)) || (rc = dalloc(&w.pend, h->WH)) ||
-            (rc = dalloc(&w.slist, std::min<int64_t>(h->WH, kCandMaxList))) || (rc = dalloc(&w.cinfo, kCiWords)))
+            (rc = dalloc(&w.slist, h->WH)) || (rc = dalloc(&w.cinfo, kCiWords)))
             return bail(rc);
-    if ((rc = dalloc(&h->cscr, (size_t)std::min(h->pool_batch, 64) * h->cslices * h->cgps * kGroupCells)))
-        return bail(rc);
+    if ((rc = dalloc(&h->cscr, (size_t)std::min(h->pool_batch, 64) * h->WH))) return bail(rc);
+    if (hipHostMalloc((void **)&h->plan_pin, 2 * sizeof(int)) != hipSuccess)
+        return bail(fail(FARMS_EHIP, "hipHostMalloc"));
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
     return FARMS_OK;
@@ -3936,6 +3987,7 @@ extern "C" int farms_destroy(farms_handle *h) {
         if (w.done) (void)hipEventDestroy(w.done);
         if (w.ready) (void)hipEventDestroy(w.ready);
         if (w.fend) (void)hipEventDestroy(w.fend);
+        if (w.plan_ev) (void)hipEventDestroy(w.plan_ev);
     }
     for (auto &ev : h->gpool)
         if (ev) (void)hipEventDestroy(ev);
@@ -3955,6 +4007,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     for (auto &ev : h->final_ev) (void)hipEventDestroy(ev);
     if (h->s_copy) (void)hipStreamDestroy(h->s_copy);
     if (h->pin_in) (void)hipHostFree(h->pin_in);
+    if (h->plan_pin) (void)hipHostFree(h->plan_pin);
     if (h->pin_out) (void)hipHostFree(h->pin_out);
     dfree(h->io_x); dfree(h->io_y); dfree(h->io_t); dfree(h->io_p); dfree(h->io_scale);
     for (auto &d : h->io_rec) dfree(d);
@@ -4001,13 +4054,7 @@ extern "C" int farms_kernel_info(const farms_handle *h, char *buf, int32_t len) 
     else if (!quad) fit = "k_fit<" + fr + ">";
     else fit = "k_fit_quad<" + fr + ">";
     // the candidate build the last pooling call took (decided on the device per call)
-    std::string cand;
-    if (h->cand_set >= 0) {
-        int flag = 0;
-        HIPCHK(hipStreamSynchronize(h->s_chain));
-        HIPCHK(hipMemcpy(&flag, h->ws[h->cand_set].cinfo + kCiFlag, sizeof(int), hipMemcpyDeviceToHost));
-        cand = flag ? "k_cand" : "k_chain";
-    }
+    const std::string cand = h->cand_last < 0 ? "" : h->cand_last ? "k_cand" : "k_chain";
     const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(fast && quad ? mode : -1) +
                            ", \"pool\": \"k_pool<" + std::to_string(h->K) + ">\", \"pool_cap\": " +
                            (pool_w7(h->fr) ? "7" : "6") + ", \"cand_last\": \"" + cand + "\"}";

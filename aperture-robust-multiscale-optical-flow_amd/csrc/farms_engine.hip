@@ -1913,18 +1913,20 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
     int k[kChainCells], kend[kChainCells], nxt[kChainCells], pnx[kChainCells];
     ChainFlow snap[kChainCells], pf[kChainCells];
     uint32_t dirty = 0;
-    // the next touch of cell i: its flow (read only when nxt[i] < lim) and the
-    // run entry after it (pnx(i) applies the run's end).  Loaded for every lane
-    // and cell slot after each chunk, from clamped indices, with no select on the
-    // loaded values: a load under a branch is waited for at the branch end, and
-    // a select right after the load waits for it too -- either serialized one
-    // round trip per cell slot and chunk; these stay in flight until the next
-    // chunk reads them (a cell that did not move reloads the same values).
+    // the next touch of cell i: its flow and the run entry after it, loaded
+    // when the cell moves.  (Round 4 tried loading them for every lane and cell
+    // slot after each chunk from clamped indices, so that no load sat under a
+    // branch: the untouched cells' loads all went to evf[0] and P[0], one L2
+    // channel, and a C3 step took 184 ms against 89.)
     auto prefetch = [&](int i) {
-        pf[i] = chain_load(&c.evf[nxt[i] < lim ? nxt[i] : 0]);
-        pnx[i] = c.P[k[i] + 1 <= kend[i] ? k[i] + 1 : 0];
+        pnx[i] = INT_MAX;
+        pf[i] = ChainFlow{0.0, 0.0, 0.0, 0u};
+        if (nxt[i] < lim) {
+            pf[i] = chain_load(&c.evf[nxt[i]]);
+            if (k[i] + 1 <= kend[i]) pnx[i] = c.P[k[i] + 1];
+        }
     };
-    auto pnext = [&](int i) { return k[i] + 1 <= kend[i] ? pnx[i] : INT_MAX; };
+    auto pnext = [&](int i) { return pnx[i]; };
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) {
         const int64_t q = (g * kChainCells + i) * 64 + lane;
@@ -2026,16 +2028,14 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
                 c.hdr_ring[kb] = hd;
                 c.val_ring[kb] = v;
             }
-            if (touched) {  // advance: snapshot <- last event of the chunk at q
+            if (touched) {  // advance: snapshot <- last event of the chunk at q; prefetch the next touch
                 snap[i] = fl;
                 k[i] = run_hi + 1;
                 nxt[i] = nn;
                 dirty |= 1u << i;
+                prefetch(i);
             }
         }
-        // the next touches, every slot's loads in flight together
-#pragma unroll
-        for (int i = 0; i < kChainCells; ++i) prefetch(i);
     }
 #pragma unroll
     for (int i = 0; i < kChainCells; ++i) {
@@ -2660,7 +2660,10 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     if (total > 0) {
         locate(0, rc, kc);
 #pragma unroll
-        for (int h = 0; h < NH; ++h) hc[h] = at32(chdr, 64 * h + lane < total ? (uint32_t)kc[h] : 0u);  // (clamped: no exec mask)
+        // (lanes past the end load lane 0's header: no exec mask, and no
+        // second line -- a fixed index would send every wave to one L2 channel)
+        for (int h = 0; h < NH; ++h)
+            hc[h] = at32(chdr, 64 * h + lane < total ? (uint32_t)kc[h] : (uint32_t)__builtin_amdgcn_readfirstlane(kc[0]));
     }
     // the previous step's contributors: ballots, values, smallest scales
     uint64_t pbal[NH];
@@ -2726,7 +2729,9 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         if (f0 + 64 * NH < total) {  // (wave-uniform)
             locate(f0 + 64 * NH, rn, kn);
 #pragma unroll
-            for (int h = 0; h < NH; ++h) hn[h] = at32(chdr, f0 + 64 * (NH + h) + lane < total ? (uint32_t)kn[h] : 0u);  // (clamped)
+            for (int h = 0; h < NH; ++h)
+                hn[h] = at32(chdr, f0 + 64 * (NH + h) + lane < total ? (uint32_t)kn[h]
+                                                                      : (uint32_t)__builtin_amdgcn_readfirstlane(kn[0]));
         }
         // ---- stage and fold the previous step's contributors
         uint64_t pany = 0;
@@ -4240,6 +4245,10 @@ extern "C" int farms_process_device(farms_handle *h, const int32_t *d_x, const i
         !d_out->r_local || !d_out->theta_local || !d_out->scale)
         return fail(FARMS_EINVAL, "null array");
     HIPCHK(hipSetDevice(h->prm.device));
+    // (Round 4: sub-batches of whole super-chunks on alternating workspace sets,
+    // so that the prep of sub-batch b + 1 ran under the pooling of b: C3 79.7 /
+    // 80.7 / 82.6 ms per step for 2 / 4 / 8 against 80.0 for one call,
+    // profiles/r04_ab_dev_subbatches.log; not kept.)
     int rc = ensure_capacity(h, h->ws[0], n);
     if (rc) return rc;
     return run_core(h, h->ws[0], d_x, d_y, d_t, d_p, n, d_out);

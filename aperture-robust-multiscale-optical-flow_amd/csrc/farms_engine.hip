@@ -3337,6 +3337,16 @@ int cand_force() {
     if (!v) return 0;
     return v[0] == 'e' ? 1 : v[0] == 'c' ? 2 : 0;
 }
+// The fit sweep on one stream or on two (even / odd chunks): two for the
+// fit-bound filters (fs 7: C4 73.4 -> 64.8 ms per step), one below, where the
+// pooling paces the step and a second fit stream takes its slots (C3 80.0 ->
+// 81.6 ms; profiles/r04_ab_fit_streams.log).  FARMS_FIT_STREAMS=1|2 overrides
+// (A/B aid, every choice gives the same bits).
+int fit_streams_for(int fr) {
+    const char *v = getenv("FARMS_FIT_STREAMS");
+    if (v && (v[0] == '1' || v[0] == '2')) return v[0] - '0';
+    return fr >= 3 ? 2 : 1;
+}
 int fit_mode_env() {
     const char *fu = getenv("FARMS_FIT_MODE");
     const int m = fu ? atoi(fu) : 1;
@@ -3455,7 +3465,7 @@ int claim_set(farms_handle *h, Work &w, int n, hipEvent_t *t_start) {
         int rc = mark(h, s, t_start);
         if (rc) return rc;
     }
-    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 3 * (size_t)n_super);
+    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
 }
 
 // The prep of a call on set w (stream F): validate, pixel ids, sort by pixel,
@@ -3557,15 +3567,12 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         if (rc) return rc;
     }
     // sync events: [0] prep done, [1 + f] fit chunk f done, then per super-chunk
-    // S: cand[S] (its candidate lists built), pool[S] (its pooling done),
-    // flow[S] (its local flows final: k_flow on F after its fits)
+    // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
     hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
     auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
-    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 3 * S]; };
-    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 3 * S]; };
-    auto ev_flow = [&](int S) { return w.sync_ev[3 + n_fit_chunks + 3 * S]; };
+    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
+    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
     auto super_end = [&](int S) { return (int)std::min<int64_t>((int64_t)(S + 1) * B * h->pool_chunk, n); };
-    int flow_next = 0;  // phase 0: the next super-chunk whose k_flow is not enqueued
     if (phase == 2) ev_prep = w.ready;  // prepared by phase 1: its fits and the imported flows are in place
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
@@ -3602,50 +3609,63 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         pr.blocks = ceil_div(std::max(pr.c1 - pr.c0, pr.c0 - pr.p0), 64);
         return pr;
     };
-    auto launch_prep = [&](const FitPrep &pr) {
-        hipLaunchKernelGGL(k_fit_prep, dim3(pr.blocks), dim3(64), 0, s, c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq);
+    // Two fit streams (fit_streams_for): chunk f runs on F (even) or F2 (odd).
+    // The fit of chunk f reads SAE buffer f % 2 only, and the prep of chunk f
+    // (into that buffer) reads nothing a fit writes (stamps and links), so the
+    // even and odd chains are independent: the prep of f + 2 waits only for the
+    // fit of f on its own stream, and a fit launch's tail overlaps the next
+    // chunk's fit instead of idling its slots.  (One stream: the prep of chunk
+    // f + 1 rides on the launch of fit f.)  F2 is the copy stream, idle in a
+    // device call after its range check: a fifth stream would share a hardware
+    // queue with one of the four (HIP maps streams onto GPU_MAX_HW_QUEUES = 4
+    // queues round-robin, and the box's runtime kept 4 whatever the variable
+    // said), serializing either the two fit streams or the host path's copies
+    // behind F's kernels (C4 73.3 ms; C3 host path 103.8 against 89.3 ms).  So
+    // the host path, which keeps the copy stream busy, runs one fit stream.
+    const bool two = !serial && !on_super && fit_streams_for(h->fr) == 2 && n_fit_chunks > 1;
+    auto fit_stream = [&](int f) { return two && (f & 1) ? h->s_copy : s; };
+    auto launch_prep = [&](const FitPrep &pr, hipStream_t st) {
+        hipLaunchKernelGGL(k_fit_prep, dim3(pr.blocks), dim3(64), 0, st, c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq);
     };
-    auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F
+    auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F (or F2)
         const int c0 = fit_start(f), c1 = fit_chunk_end(f);
-        if (f == 0) launch_prep(prep_of(0));
+        hipStream_t sf = fit_stream(f);
+        if (two && f == 1) HIPCHK(hipStreamWaitEvent(sf, w.sync_ev[0], 0));  // F2 starts behind the call's prep
+        if (f == 0 || two) launch_prep(prep_of(f), sf);
         Ctx cf = c;
         cf.cells = cells_of(f);
         FitPrep next{};
-        if (f + 1 < n_fit_chunks) next = prep_of(f + 1);
+        if (!two && f + 1 < n_fit_chunks) next = prep_of(f + 1);
         hipEvent_t k0 = nullptr, k1 = nullptr;
-        if (prof && h->fit_events) { int rc = mark(h, s, &k0); if (rc) return rc; }
+        if (prof && h->fit_events) { int rc = mark(h, sf, &k0); if (rc) return rc; }
         bool merged = false;
         if (fast_fit) {
-            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, s, fit_quad, fit_mode, next);
+            merged = launch_fit(cf, h->fr, c0, c1, seq_base + f + 1, sf, fit_quad, fit_mode, next);
         } else {  // no per-thread fast path for this filter: every event wave-cooperative
-            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, s, cf, seq_base + f + 1, w.Q + c0,
+            hipLaunchKernelGGL(k_fit_wave, dim3(kFitWaveBlocks), dim3(256), 0, sf, cf, seq_base + f + 1, w.Q + c0,
                                c1 - c0);
         }
-        if (!merged && next.blocks > 0) launch_prep(next);
+        if (!merged && next.blocks > 0) launch_prep(next, sf);
         if (k0) {
-            int rc = mark(h, s, &k1);
+            int rc = mark(h, sf, &k1);
             if (rc) return rc;
             h->brk.push_back({k0, k1, kBrFitKernel});
         }
-        HIPCHK(hipEventRecord(ev_fit(f), s));
         ++fit_launches;
-        // the local flows of every super-chunk whose fits are now all enqueued,
-        // on F right behind them (one-wave blocks: they take slots as the
-        // pooling waves free them), so that the chain stream only waits for them
-        while (phase == 0 && flow_next < n_super && (f == n_fit_chunks - 1 || c1 >= super_end(flow_next))) {
-            const int q0 = flow_next * B * h->pool_chunk, q1 = super_end(flow_next);
-            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 64)), dim3(64), 0, s, c, q0, q1);
-            HIPCHK(hipEventRecord(ev_flow(flow_next), s));
-            ++flow_next;
-        }
         if (f == n_fit_chunks - 1) {  // the SAE after the call in both buffers (streaming state)
             FitPrep fin{cells_of(f), c0, n, n, 0u, 0};
             fin.blocks = ceil_div(n - c0, 64);
-            launch_prep(fin);
+            launch_prep(fin, sf);
+            // buffer (f + 1) % 2: its last reader is the fit of chunk f - 1
+            if (two) HIPCHK(hipStreamWaitEvent(sf, ev_fit(f - 1), 0));
             fin.cells = cells_of(f + 1);
             fin.p0 = fit_start(std::max(f - 1, 0));
             fin.blocks = ceil_div(n - fin.p0, 64);
-            launch_prep(fin);
+            launch_prep(fin, sf);
+        }
+        HIPCHK(hipEventRecord(ev_fit(f), sf));
+        if (f == n_fit_chunks - 1) {
+            if (sf != s) HIPCHK(hipStreamWaitEvent(s, ev_fit(f), 0));  // F holds the whole sweep from here on
             if (t_prep && phase == 0) {  // the fit sweep's bracket (phase 1 closes it after k_flow)
                 hipEvent_t e2 = nullptr;
                 int rc = mark(h, s, &e2);
@@ -3710,9 +3730,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
         if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
-        // the chain reads the local flows of every event of the super-chunk
-        // (phase 2: final since phase 1)
-        if (phase == 0) HIPCHK(hipStreamWaitEvent(sc, ev_flow(S), 0));
+        if (phase == 0) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
+            const int fl = std::min((int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk), n_fit_chunks - 1);
+            HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0));
+            if (two && fl >= 1) HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl - 1), 0));  // the other fit stream
+            const int q0 = ch0 * h->pool_chunk, q1 = super_end(S);
+            // one-wave blocks: they take slots as the pooling waves free them
+            hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 64)), dim3(64), 0, sc, c, q0, q1);
+        }
         if (use_cand < 0) { int rc = decide_cand(); if (rc) return rc; }
         for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (k_chain: their spans in one VGPR)
             const int b = std::min(a + 64, ch1);
@@ -3945,7 +3970,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         (pool_mask.empty()
              ? hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo)
              : hipExtStreamCreateWithCUMask(&h->s_pool, (uint32_t)pool_mask.size(), pool_mask.data())) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->s_copy, hipStreamNonBlocking) != hipSuccess)
+        hipStreamCreateWithPriority(&h->s_copy, hipStreamNonBlocking, prio_hi) != hipSuccess)  // (device calls: odd fits)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {
         std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end,

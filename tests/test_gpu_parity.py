@@ -258,14 +258,18 @@ def test_out_of_sensor_event_is_rejected():
 def test_fit_variants_are_bitwise_identical(fs, monkeypatch):
     """The quad-lane fits (FARMS_FIT_MODE 0: re-gathered winning window, 1:
     union tile by columns, 2: union tile by rows) and the one-thread fit
-    evaluate the same arithmetic in the same order: bitwise-equal records."""
+    evaluate the same arithmetic in the same order: bitwise-equal records.
+    The sweep on one fit stream or two (FARMS_FIT_STREAMS, even / odd chunks;
+    small fit chunks so that there are many of each) gives the same bits."""
     ev = farms.synth_config(3, 150_000)
     x, y, t, p = ev.relative()
     outs = []
-    for quad, mode in [("1", "1"), ("1", "0"), ("1", "2"), ("0", "1")]:
+    for quad, mode, streams, fc in [("1", "1", "2", 0), ("1", "0", "2", 0), ("1", "2", "2", 0), ("0", "1", "2", 0),
+                                    ("1", "1", "1", 0), ("1", "1", "1", 8192), ("1", "1", "2", 8192)]:
         monkeypatch.setenv("FARMS_FIT_QUAD", quad)
         monkeypatch.setenv("FARMS_FIT_MODE", mode)
-        with farms.FlowManager(720, 1280, fs, 5) as fm:
+        monkeypatch.setenv("FARMS_FIT_STREAMS", streams)
+        with farms.FlowManager(720, 1280, fs, 5, fit_chunk=fc) as fm:
             outs.append(fm.process(x, y, t, p))
     for o in outs[1:]:
         assert bitwise_equal(outs[0], o)

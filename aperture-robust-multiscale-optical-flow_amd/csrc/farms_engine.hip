@@ -491,7 +491,10 @@ __global__ void k_pool_desc(Ctx c, int p0, int p1) {
 // wave opens with one 16-B load where it needed two dependent round trips (Q,
 // then the event's fields).  After the work-order sort, in prep.
 __global__ void k_fit_desc(Ctx c) {
-    const int w = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    // XCD-contiguous blocks: a pooling chunk's gathers of x, y, t (its events
+    // are a 8,192-event window) stay in one L2 instead of being fetched by all
+    // eight (2.4 GB of fetches for 50M events with round-robin blocks, PMC)
+    const int w = (int)(work_block() * blockDim.x + threadIdx.x);
     if (w >= c.n) return;
     const int e = c.Q[w];
     c.fdesc[w] = make_int4(e, c.x[e], c.y[e], (int)c.t[e]);
@@ -2371,12 +2374,15 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
 }
 
 // After a call's last k_cand: every cell's flow snapshot becomes its last
-// event's flow (k_chain advances them itself).
+// event's flow, P[pend[q]] (k_chain advances them itself).  One thread per
+// cell: 4 B per cell plus two gathers per touched cell, where a pass over the
+// events' links read 16 B per event (0.96 GB per 50M-event call, PMC).
 __global__ void k_cand_commit(Ctx c) {
-    const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (e >= c.n || c.link[e].z != INT_MAX) return;
-    const uint32_t q = c.pix[e];
-    FlowCell f = c.evf[e];
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= c.WH) return;
+    const int k = c.pend[q];
+    if (k < 0) return;
+    FlowCell f = c.evf[c.P[k]];
     f.pad = 0;
     c.fsnap[q] = f;
     c.ftime[q] = f.L > 0 ? (int64_t)f.t : -1;
@@ -3777,7 +3783,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     h->super_base += n_super;
     h->chunk_base += n_pool_chunks;
     if (n_super > 0) {  // k_cand calls: the snapshots advance to the call's last events
-        if (use_cand == 1) hipLaunchKernelGGL(k_cand_commit, dim3(ceil_div(n, 256)), dim3(256), 0, sc, c);
+        if (use_cand == 1) hipLaunchKernelGGL(k_cand_commit, dim3(ceil_div(h->WH, 256)), dim3(256), 0, sc, c);
         HIPCHK(hipEventRecord(h->chain_end, sc));
     }
     HIPCHK(hipGetLastError());

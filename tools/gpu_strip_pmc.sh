@@ -14,7 +14,7 @@ LABEL="tools/strip_rank.py $ARGS"
 timeout -k 10 600 python3 -u tools/strip_rank.py $ARGS > gpurun_out/strip_pmc_prep.log 2>&1
 rc=$?; echo "halo prep rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_pool|k_fit|k_chain" -d gpurun_out/spmc_$C -o pmc \
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_pool|k_fit|k_chain|k_cand|k_flow" -d gpurun_out/spmc_$C -o pmc \
      --output-format csv -- python3 tools/strip_rank.py $ARGS > gpurun_out/spmc_$C.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
@@ -22,7 +22,7 @@ python3 tools/traffic.py gpurun_out/spmc_FETCH_SIZE/pmc_counter_collection.csv \
    gpurun_out/spmc_WRITE_SIZE/pmc_counter_collection.csv --label "$LABEL" > gpurun_out/traffic_c${CFG}_strips.json
 rc=$?; echo "traffic rc=$rc"; [ $rc -ne 0 ] && exit $rc
 CTRS="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD"
-timeout -k 10 600 rocprofv3 --pmc $CTRS --kernel-include-regex "k_pool|k_fit|k_chain" -d gpurun_out/spmc_sq -o pmc \
+timeout -k 10 600 rocprofv3 --pmc $CTRS --kernel-include-regex "k_pool|k_fit|k_chain|k_cand|k_flow" -d gpurun_out/spmc_sq -o pmc \
    --output-format csv -- python3 tools/strip_rank.py $ARGS > gpurun_out/spmc_sq.log 2>&1
 rc=$?; echo "pmc sq rc=$rc"; [ $rc -ne 0 ] && exit $rc
 python3 tools/sq_summary.py gpurun_out/spmc_sq/pmc_counter_collection.csv --label "$LABEL" \

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=${TRAFFIC_OUT:-gpurun_out/traffic_c3.json}
 ARGS="--steps 1 --warmup 0 --no-cpu-baseline --host-steps 0 ${BENCH_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_pool|k_fit|k_chain" -d gpurun_out/pmc_$C -o pmc \
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "k_pool|k_fit|k_chain|k_cand|k_flow" -d gpurun_out/pmc_$C -o pmc \
      --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc_$C.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"
   [ $rc -ne 0 ] && exit $rc

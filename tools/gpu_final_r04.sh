@@ -6,6 +6,7 @@
 #   suite, smoke, the bench lines of C3 (with the CPU baseline and the host
 #   path), C4, C2, C5, a rocprofv3 --kernel-trace --stats summary of the C3
 #   bench command, and the N=2 rehearsals of both splits (gloo, one GPU).
+#   ONLY_PMC=1: the PMC passes only; SKIP_PMC=1 / SKIP_TESTS=1: skip those.
 cd /root/repo
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -15,6 +16,7 @@ if [ "${SKIP_PMC:-0}" != "1" ]; then
   CFGS="${PMC_CFGS:-3 4 2 5}" R=$R bash tools/gpu_pmc_configs.sh > gpurun_out/final_pmc.out 2>&1
   step pmc $?
   cp gpurun_out/${R}_traffic_c*.json gpurun_out/${R}_sq_c*.json profiles/
+  [ "${ONLY_PMC:-0}" = "1" ] && { rm -rf gpurun_out/pmc_*; exit 0; }
 fi
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   timeout -k 10 1200 python -u -m pytest tests -v -m gpu -rA --timeout 400 --timeout-method thread \

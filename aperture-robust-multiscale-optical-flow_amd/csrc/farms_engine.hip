@@ -170,7 +170,9 @@ constexpr int64_t kMaxSlots = (int64_t(1) << 24) - 256;
 // Mevents/s, round 3)
 constexpr int kPoolHalves = 1;
 // k_pool staging: {L, L cos, L sin, 1} and k0 of the 64 x kPoolHalves entries of a step, 8-B words
-constexpr int kPoolValWords = (4 * 64 + 8) * kPoolHalves;
+// plus 8 slots for the entries a step carries to the next (the fold takes whole groups of 8)
+constexpr int kPoolSlots = 64 * kPoolHalves + 8;
+constexpr int kPoolValWords = 4 * kPoolSlots + kPoolSlots / 8;
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
 
 struct Ctx {
@@ -2638,7 +2640,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     const int kk = lane - grp * K;
     constexpr int NH = kPoolHalves;  // candidates per lane per step: a step covers 64 * NH positions
 #pragma unroll
-    for (int h = 0; h < NH; ++h) s_val[4 * (lane + 64 * h) + 3] = 1.0;  // the count's "value" (staging never overwrites it)
+    for (int i = lane; i < kPoolSlots; i += 64) s_val[4 * i + 3] = 1.0;  // the count's "value" (staging never overwrites it)
     const uint64_t lt = (1ull << lane) - 1;
     double acc = 0.0;
     int ncon_total = 0;
@@ -2677,6 +2679,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     int pk0[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) { pbal[h] = 0; pv[h][0] = pv[h][1] = pv[h][2] = 0.0; pk0[h] = K; }
+    int staged = 0;  // (wave-uniform) staged entries not yet folded, at slots [0, staged)
     for (int f0 = 0;; f0 += 64 * NH) {
         const bool have = f0 < total;  // wave-uniform
         bool con[NH];
@@ -2739,41 +2742,61 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 hn[h] = at32(chdr, f0 + 64 * (NH + h) + lane < total ? (uint32_t)kn[h]
                                                                       : (uint32_t)__builtin_amdgcn_readfirstlane(kn[0]));
         }
-        // ---- stage and fold the previous step's contributors
+        // ---- stage and fold the previous step's contributors: they go to LDS
+        // slots [staged, staged + cnt) in raster order (half 0 before half 1),
+        // behind the entries the last step left unfolded; whole groups of 8
+        // are folded and the rest (< 8) moves to slots [0, ...) for the next
+        // step, so that only the event's last group is padded (every step's
+        // last group was, before: ~8% of the fold's adds at C3)
         uint64_t pany = 0;
 #pragma unroll
         for (int h = 0; h < NH; ++h) pany |= pbal[h];
         if (pany) {
-            // every lane writes one slot per half: the contributors first, in
-            // raster order (half 0 before half 1), then the others with k0 = K
-            // (in no scale)
             int cntb[NH], cnt = 0;
 #pragma unroll
             for (int h = 0; h < NH; ++h) { cntb[h] = (int)__popcll(pbal[h]); cnt += cntb[h]; }
             // the previous fold's LDS reads are done (wave-private LDS)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            int cbase = 0, nbase = cnt;
+            int cbase = staged;
 #pragma unroll
             for (int h = 0; h < NH; ++h) {
-                const bool pc = (pbal[h] >> lane) & 1;
-                const int slot = pc ? cbase + (int)__popcll(pbal[h] & lt) : nbase + (int)__popcll(~pbal[h] & lt);
-                s_val[4 * slot] = pv[h][0]; s_val[4 * slot + 1] = pv[h][1]; s_val[4 * slot + 2] = pv[h][2];
-                s_k0[slot] = (uint8_t)(pc ? pk0[h] : K);
+                if ((pbal[h] >> lane) & 1) {
+                    const int slot = cbase + (int)__popcll(pbal[h] & lt);
+                    s_val[4 * slot] = pv[h][0]; s_val[4 * slot + 1] = pv[h][1]; s_val[4 * slot + 2] = pv[h][2];
+                    s_k0[slot] = (uint8_t)pk0[h];
+                }
                 cbase += cntb[h];
-                nbase += 64 - cntb[h];
             }
+            staged = cbase;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            const int whole = staged & ~7;
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
 #pragma unroll 1
-            for (int r = 0; r < cnt; r += 8) {  // slots past cnt: k0 = K (in no scale)
+            for (int r = 0; r < whole; r += 8) {
                 const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
                 double vv[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
                 fold8(acc, kk, kw0, kw1, vv);
             }
+            if (whole > 0 && staged > whole) {  // carry the rest to slots [0, staged - whole)
+                const int rest = staged - whole;
+                double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+                uint8_t mk = (uint8_t)K;
+                if (lane < rest) {
+                    m0 = s_val[4 * (whole + lane)]; m1 = s_val[4 * (whole + lane) + 1]; m2 = s_val[4 * (whole + lane) + 2];
+                    mk = s_k0[whole + lane];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (lane < rest) {
+                    s_val[4 * lane] = m0; s_val[4 * lane + 1] = m1; s_val[4 * lane + 2] = m2;
+                    s_k0[lane] = mk;
+                }
+            }
+            staged -= whole;
             ncon_total += cnt;
         }
         if (!have) break;
@@ -2784,6 +2807,19 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             pk0[h] = k0[h];
             hc[h] = hn[h]; rc[h] = rn[h]; kc[h] = kn[h];
         }
+    }
+    if (staged > 0) {  // the last group, padded with entries in no scale (k0 = K)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= staged && lane < 8) s_k0[lane] = (uint8_t)K;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+        const uint32_t kw0 = k4p[0], kw1 = k4p[1];
+        double vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * u + grp];
+        fold8(acc, kk, kw0, kw1, vv);
     }
     pool_finish<K>(c, e, lane, acc, total, ncon_total);
 }
@@ -2858,7 +2894,7 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     uint64_t *s_start = s_dyn;
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
-    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * 64 * kPoolHalves);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * kPoolSlots);
     const int w = c0 + work_block();
     if (w >= c1) return;
     // the event and its fields in one 16-B load (k_pool_desc)

@@ -2888,7 +2888,7 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     // waves/SIMD won while the fit carried the libm chain (C3: 6 waves 109.9 ms
     // per step, 7: 122.0, 5: 113.9); with k_flow split out, C3 runs 7 waves in
     // 86.7-87.2 ms, 6: 89.9-90.3, 8 (64 VGPRs, 5 spills): 101.9, 5: 96.4; the
-    // heavier fs-7 fit (C4/C5) still wants 6 (pool_for).
+    // heavier fs-7 fit (C4/C5) wanted 6 until its sweep ran on two streams (pool_for).
     if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
     else asm volatile("" ::: FARMS_POOL_FLOOR_6);
     uint64_t *s_start = s_dyn;
@@ -3351,10 +3351,12 @@ pool_launcher pool_for_cap(int K) {
     }
 }
 // k_pool's occupancy cap by the fit's weight (see k_pool): 7 waves per SIMD
-// beside the fs <= 5 fits, 6 beside the heavier fs-7 and wave fits;
-// FARMS_POOL_CAP=6|7 overrides (tuning aid).
+// beside the quad fits (fs <= 7), 6 beside the wave fits of larger filters.
+// (fs 7 wanted 6 while its fit ran on one stream; on two, 7 wins: C4 63.4
+// against 64.6 ms, C5 73.5 against 76.4 on a 50M-event share,
+// profiles/r04_ab_pool_cap_fs7.log.)  FARMS_POOL_CAP=6|7 overrides (tuning aid).
 bool pool_w7(int fr) {
-    bool w7 = fr <= 2;
+    bool w7 = fr <= 3;
     if (const char *v = getenv("FARMS_POOL_CAP")) w7 = v[0] == '7';
     return w7;
 }

@@ -3509,7 +3509,7 @@ int claim_set(farms_handle *h, Work &w, int n, hipEvent_t *t_start) {
         int rc = mark(h, s, t_start);
         if (rc) return rc;
     }
-    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 2 * (size_t)n_super);
+    return ensure_sync_events(w, 1 + (size_t)n_fit_chunks + 3 * (size_t)n_super);
 }
 
 // The prep of a call on set w (stream F): validate, pixel ids, sort by pixel,
@@ -3614,9 +3614,10 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     // S: cand[S] (its candidate lists built), pool[S] (its pooling done)
     hipEvent_t ev_prep = w.sync_ev[0];  // (phase 2: w.ready)
     auto ev_fit = [&](int f) { return w.sync_ev[1 + f]; };
-    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 2 * S]; };
-    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 2 * S]; };
+    auto ev_cand = [&](int S) { return w.sync_ev[1 + n_fit_chunks + 3 * (size_t)S]; };
+    auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 3 * (size_t)S]; };
     auto super_end = [&](int S) { return (int)std::min<int64_t>((int64_t)(S + 1) * B * h->pool_chunk, n); };
+    auto ev_pk = [&](int S) { return w.sync_ev[3 + n_fit_chunks + 3 * (size_t)S]; };  // k_pool(S) done
     if (phase == 2) ev_prep = w.ready;  // prepared by phase 1: its fits and the imported flows are in place
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
@@ -3632,6 +3633,22 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     const char *ser = getenv("FARMS_SERIALIZE");
     const bool serial = ser && ser[0] == '1';
     hipStream_t sc = serial ? s : h->s_chain, sp = serial ? s : h->s_pool;
+    const int64_t sb0 = h->super_base;
+    // (Gx, Gy) -> (RTrue, ThetaTrue) of super-chunk T on the chain stream once
+    // its k_pool is done; then its records are final (round 4: k_true_polar
+    // off the pooling stream, which paces the step at C3; the chain stream,
+    // one super-chunk ahead, has the slack)
+    auto finish_super = [&](int T) -> int {
+        const int q0 = T * B * h->pool_chunk, q1 = super_end(T);
+        HIPCHK(hipStreamWaitEvent(sc, ev_pk(T), 0));
+        launch_true_polar(h, c, sc, sb0 + T, q0, q1);
+        if (int rc = record_pool_done(h, sc, sb0 + T, ev_pool(T))) return rc;
+        if (on_super) {
+            int rc = (*on_super)(T, q0, q1, ev_pool(T));
+            if (rc) return rc;
+        }
+        return FARMS_OK;
+    };
     pool_launcher pl = pool_for(h->K, h->fr);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const bool fit_quad = fit_quad_env();
@@ -3806,14 +3823,12 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             if (rc) return rc;
             h->brk.push_back({k0, k1, kBrPoolKernel});
         }
-        // (Gx, Gy) -> (RTrue, ThetaTrue): the super-chunk's records are final
-        launch_true_polar(h, c, sp, Sg, p0, p1);
-        if (int rc = record_pool_done(h, sp, Sg, ev_pool(S))) return rc;
-        if (on_super) {
-            int rc = (*on_super)(S, p0, p1, ev_pool(S));
-            if (rc) return rc;
-        }
+        HIPCHK(hipEventRecord(ev_pk(S), sp));
+        // the previous super-chunk's records, on the chain stream behind this
+        // one's candidate lists: stream P runs nothing but k_pool
+        if (S > 0) { int rc = finish_super(S - 1); if (rc) return rc; }
     }
+    if (n_super > 0) { int rc = finish_super(n_super - 1); if (rc) return rc; }
     while (fit_enqueued < n_fit_chunks) {
         int rc = enqueue_fit(fit_enqueued++);
         if (rc) return rc;
@@ -4649,7 +4664,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             // an event of the call's own (the set's pooling events are recorded again by later sub-batches)
             if ((int64_t)h->final_ev.size() <= S_all || (int64_t)h->copy_ev.size() <= S_all)
                 return fail(FARMS_EHIP, "farms_process: super-chunk count");
-            HIPCHK(hipEventRecord(h->final_ev[S_all], h->s_pool));
+            HIPCHK(hipEventRecord(h->final_ev[S_all], h->polar_stream));  // where its k_true_polar ran
             {
                 std::lock_guard<std::mutex> lk(dmu);
                 dq.push_back(Download{S_all, a0, p0, p1, h->final_ev[S_all]});

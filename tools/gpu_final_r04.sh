@@ -29,7 +29,7 @@ fi
 timeout -k 10 600 python -u bench.py --config 3 > gpurun_out/${R}_bench_c3.log 2>&1
 step bench_c3 $?
 for C in 4 2 5; do
-  timeout -k 10 600 python -u bench.py --config $C --no-cpu-baseline --host-steps 0 > gpurun_out/${R}_bench_c$C.log 2>&1
+  timeout -k 10 600 python -u bench.py --config $C --host-steps 0 > gpurun_out/${R}_bench_c$C.log 2>&1
   step bench_c$C $?
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \

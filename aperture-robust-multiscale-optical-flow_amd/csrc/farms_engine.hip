@@ -1857,12 +1857,11 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
 constexpr int kGroupCells = 256;
 
 // The call's candidate-build plan (Ctx::cinfo, per workspace set):
-//   kCiFlag     (unused)
 //   kCiMaxBack  largest chunk distance back to cbk (k_cand_plan_back)
 //   kCiCount    call-start snapshot list length (k_cand_list)
 //   kCiLMin/Max stamp range of that list
 //   kCiTMin/Max stamp range of the call's events
-enum { kCiFlag = 0, kCiMaxBack, kCiCount, kCiLMin, kCiLMax, kCiTMin, kCiTMax, kCiWords };
+enum { kCiMaxBack = 0, kCiCount, kCiLMin, kCiLMax, kCiTMin, kCiTMax, kCiWords };
 // k_cand takes a call when every chunk's kill window reaches back at most this
 // many chunks (a time-ordered stream: 2-3); other streams (out-of-order stamps)
 // keep k_chain, whose cost is independent of the order.  The host reads the
@@ -2114,7 +2113,6 @@ __global__ __launch_bounds__(1024) void k_cand_plan_max(const uint32_t *tmin, co
         __syncthreads();
     }
     if (tid == 0) {
-        info[kCiFlag] = 0;
         info[kCiMaxBack] = 0;
         info[kCiCount] = 0;
         info[kCiLMin] = (int)0xFFFFFFFFu;

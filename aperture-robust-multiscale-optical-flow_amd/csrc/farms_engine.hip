@@ -30,6 +30,7 @@
 // rounded atan2 / sin / cos (farms_libm.h); see DESIGN.md §3.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <hipcub/block/block_radix_sort.hpp>
 
 #include <algorithm>
 #include <numeric>
@@ -2172,6 +2173,79 @@ __global__ void k_cand_list(Ctx c, int4 *list) {
     }
 }
 
+// The work order of one pooling chunk per workgroup (round 4): its events'
+// 8x8-tile keys sorted in LDS by a block radix sort (stable, so events of a
+// tile stay in index order: the same Q as the device-wide sort of (chunk, tile)
+// keys), and in the same pass the fit descriptors {event, x, y, t} (gathers
+// inside the chunk's window), the column bands' work-order starts (k_cand)
+// and the chunk's stamp span.  Replaces the second device-wide radix sort,
+// k_fit_desc, k_band_starts and k_chunk_minmax for pooling chunks of 2,048,
+// 4,096 and 8,192 events (C3 77.6-77.8 -> 77.2 ms per step,
+// profiles/r04_ab_chunk_order.log).
+template <int THREADS, int ITEMS>
+__global__ __launch_bounds__(THREADS) void k_chunk_order(Ctx c, int tile_bits, int32_t *Q, int32_t *bstart,
+                                                         uint32_t *tmin, uint32_t *tmax) {
+    using BRS = hipcub::BlockRadixSort<uint32_t, THREADS, ITEMS, int>;
+    __shared__ typename BRS::TempStorage s_sort;
+    __shared__ uint32_t s_last[THREADS];
+    __shared__ uint32_t s_lo[THREADS / 64], s_hi[THREADS / 64];
+    const int ch = (int)blockIdx.x, tid = (int)threadIdx.x;
+    const int cs = ch * c.C2, cnt = min(c.C2, c.n - cs);
+    const uint32_t pad = 1u << tile_bits;
+    uint32_t key[ITEMS];
+    int val[ITEMS];
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int r = tid * ITEMS + i;
+        val[i] = r;
+        key[i] = pad;
+        if (r < cnt) {
+            const int e = cs + r;
+            const int x = c.x[e], y = c.y[e];
+            const uint32_t t = c.t[e];
+            key[i] = (uint32_t)((x - c.X0) >> c.tshift) * (uint32_t)c.tilesH + (uint32_t)(y >> c.tshift);
+            lo = t < lo ? t : lo;
+            hi = t > hi ? t : hi;
+        }
+    }
+    BRS(s_sort).Sort(key, val, 0, tile_bits + 1);
+    // blocked output: thread tid holds ranks tid * ITEMS + i, ascending
+    s_last[tid] = key[ITEMS - 1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+    }
+    if ((tid & 63) == 0) { s_lo[tid >> 6] = lo; s_hi[tid >> 6] = hi; }
+    __syncthreads();
+    const int tpb = c.bandc >> c.tshift;  // tile columns per band
+    auto band = [&](uint32_t k) { return k >= pad ? c.nbands : (int)(k / (uint32_t)c.tilesH) / tpb; };
+    int32_t *bs = bstart + (int64_t)ch * (c.nbands + 1);
+    int prev = tid > 0 ? band(s_last[tid - 1]) : -1;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int r = tid * ITEMS + i;
+        const int b = band(key[i]);
+        // the first rank of each band (padding ranks have band nbands: its start is cnt)
+        for (int q = prev + 1; q <= b; ++q) bs[q] = cs + min(r, cnt);
+        prev = b;
+        if (r < cnt) {
+            const int e = cs + val[i];
+            Q[cs + r] = e;
+            c.fdesc[cs + r] = make_int4(e, c.x[e], c.y[e], (int)c.t[e]);
+        }
+    }
+    if (tid == THREADS - 1)  // bands past the last key (no padding when the chunk is full)
+        for (int q = prev + 1; q <= c.nbands; ++q) bs[q] = cs + cnt;
+    if (tid == 0) {
+        uint32_t a = s_lo[0], b = s_hi[0];
+        for (int u = 1; u < THREADS / 64; ++u) { a = min(a, s_lo[u]); b = max(b, s_hi[u]); }
+        tmin[ch] = a;
+        tmax[ch] = b;
+    }
+}
+
 // Work-order bounds of the column bands (k_cand): the work order Q is sorted by
 // (pooling chunk, 8x8 tile), tiles x-major, so the events of chunk ch in the
 // band of columns [b * bandc, (b + 1) * bandc) are the positions
@@ -3372,6 +3446,12 @@ bool fit_quad_env() {
     const char *fq = getenv("FARMS_FIT_QUAD");
     return !(fq && fq[0] == '0');
 }
+// FARMS_ORDER=sort: the work order by the device-wide radix sort even where
+// k_chunk_order covers the pooling chunk (A/B and test aid; same bits)
+bool order_by_chunk() {
+    const char *v = getenv("FARMS_ORDER");
+    return !(v && v[0] == 's');
+}
 // FARMS_CAND=events|chain: force the candidate build (A/B and test aid; every
 // choice gives the same bits); default: k_cand for time-local streams.
 int cand_force() {
@@ -3540,17 +3620,37 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     // previous call's chain is done
     if (c.serial && h->super_base > 0) HIPCHK(hipStreamWaitEvent(s, h->chain_end, 0));
     hipLaunchKernelGGL(k_link, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.link, w.PT, h->prm.serial != 0);
-    {
+    // the work order, fit descriptors, band starts and chunk spans: one
+    // workgroup per pooling chunk when a template covers the chunk size
+    // (FARMS_ORDER=sort: the device-wide path, A/B and test aid)
+    bool ordered = false;
+    if (order_by_chunk()) {
+        const dim3 g(n_pool_chunks);
+        switch (h->pool_chunk) {
+        case 2048: hipLaunchKernelGGL((k_chunk_order<256, 8>), g, dim3(256), 0, s, c, h->tile_bits, w.Q, w.bstart,
+                                      w.ctmin, w.ctmax); ordered = true; break;
+        case 4096: hipLaunchKernelGGL((k_chunk_order<512, 8>), g, dim3(512), 0, s, c, h->tile_bits, w.Q, w.bstart,
+                                      w.ctmin, w.ctmax); ordered = true; break;
+        case 8192: hipLaunchKernelGGL((k_chunk_order<1024, 8>), g, dim3(1024), 0, s, c, h->tile_bits, w.Q, w.bstart,
+                                      w.ctmin, w.ctmax); ordered = true; break;
+        // (16,384-event chunks, fs 7: a 1024 x 16 build -- 123 VGPRs, 70 KB of LDS -- took C4 from
+        // 62.3-62.5 to 63.2-64.3 ms per step; those keep the device-wide sort)
+        default: break;
+        }
+    }
+    if (!ordered) {
         int cb = 1;
         while ((1 << cb) < n_pool_chunks) ++cb;
         if (cb + h->tile_bits > 32) return fail(FARMS_EINVAL, "too many pooling chunks for one call; raise pool_chunk");
         size_t b2 = w.cub_bytes;
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, b2, w.wkey, w.wkey_sorted, w.iota, w.Q, n, 0,
                                                   h->tile_bits + cb, s));
+        hipLaunchKernelGGL(k_fit_desc, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
+        hipLaunchKernelGGL(k_band_starts, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.wkey_sorted, h->tile_bits,
+                           w.bstart);
+        hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin,
+                           w.ctmax);
     }
-    hipLaunchKernelGGL(k_fit_desc, dim3(ceil_div(n, 256)), dim3(256), 0, s, c);
-    hipLaunchKernelGGL(k_band_starts, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.wkey_sorted, h->tile_bits, w.bstart);
-    hipLaunchKernelGGL(k_chunk_minmax, dim3(n_pool_chunks), dim3(256), 0, s, dt, n, h->pool_chunk, w.ctmin, w.ctmax);
     if (n_pool_chunks > 0) {  // the candidate build's plan: how far back each chunk's kill window reaches
         hipLaunchKernelGGL(k_cand_plan_max, dim3(1), dim3(1024), 0, s, w.ctmin, w.ctmax, n_pool_chunks, w.cpmax,
                            w.cinfo);

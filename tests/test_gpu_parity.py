@@ -543,3 +543,24 @@ def test_candidate_builds_are_bitwise_identical(monkeypatch):
             assert used == want, (name, mode, used)
         for mode in ("events", "chain"):
             assert bitwise_equal(outs[""], outs[mode]), (name, mode, compare(outs[""], outs[mode]))
+
+
+def test_work_order_builds_are_bitwise_identical(monkeypatch):
+    """The work order (tile-sorted events of each pooling chunk), the fit
+    descriptors, the column-band starts and the chunk spans come from one
+    workgroup per chunk (k_chunk_order, pooling chunks of 2,048 / 4,096 / 8,192
+    events) or from the device-wide sort (FARMS_ORDER=sort; any other chunk
+    size, e.g. fs 7's 16,384): the same bits for every chunk size either way."""
+    ev = farms.synth_config(3, 150_000)
+    x, y, t, p = ev.relative()
+    outs = []
+    for pc in (2048, 4096, 8192, 16384):
+        for order in ("", "sort"):
+            if order:
+                monkeypatch.setenv("FARMS_ORDER", order)
+            else:
+                monkeypatch.delenv("FARMS_ORDER", raising=False)
+            with farms.FlowManager(720, 1280, 5, 5, pool_chunk=pc) as fm:
+                outs.append(fm.process(x, y, t, p))
+    for o in outs[1:]:
+        assert bitwise_equal(outs[0], o)

@@ -4056,7 +4056,9 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     h->WH = (int64_t)h->WR * prm->height;
     h->J = prm->window_jump; h->M = prm->max_window; h->K = K;
     if (h->fr == 3) {  // fs 7 (169-cell fits, fewer valid events): measured best at C4, -10% per step
-        h->fit_chunk = 2 * kDefaultFitChunk;
+        // (fit chunks stay at the default: 131,072 won while the fit ran on one
+        // stream; on two, 65,536 does -- C4 61.0-61.7 against 63.5-63.7 ms, C5
+        // 181.5 against 186.2, 32,768: 64.1 / 188.3; profiles/r04_ab_fit_chunk_fs7.log)
         h->pool_chunk = 2 * kDefaultPoolChunk;
         h->pool_batch = kDefaultPoolBatch / 2;
     }

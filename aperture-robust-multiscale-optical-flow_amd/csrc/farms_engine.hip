@@ -175,6 +175,15 @@ constexpr int kPoolHalves = 1;
 constexpr int kPoolSlots = 64 * kPoolHalves + 8;
 constexpr int kPoolValWords = 4 * kPoolSlots + kPoolSlots / 8;
 constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; a row spans <= 2 candidate groups)
+// k_pool's fold lanes (round 5): lane 4 kk + g holds quantity g of scale kk, so
+// the members of an entry (scales k0..K-1) are the lanes >= 4 k0 and its mask
+// comes from the scalar unit (fold8_salu).  Needs 4K < 64: the padding entries'
+// 4K then selects junk lanes only.  Above (K = 16) the v_cmp fold (lane g K + kk).
+#ifndef FARMS_POOL_SALU
+#define FARMS_POOL_SALU 1  // tuning builds: 0 = the round-4 v_cmp fold for every K
+#endif
+template <int K>
+constexpr bool kSaluFold = FARMS_POOL_SALU && 4 * K < 64;
 
 struct Ctx {
     int W, H, n;
@@ -219,7 +228,6 @@ struct Ctx {
     int NB, C2;            // ring size, events per pooling chunk
     int ring0;             // ring buffer of the call's first pooling chunk (chunk numbers continue across calls)
     int pool_bw, pool_rs;  // k_pool LDS per wave, in 8-B words: bitmap words, row segments
-    int fit_band;          // fit blocks per pooling chunk for the band block mapping (0: runs of 8 per XCD)
     const uint32_t *ctmin, *ctmax;  // per pooling chunk
     // event-driven candidate build (k_cand): per pooling chunk the first chunk
     // whose events can still be snapshots inside its kill window (cbk), the
@@ -338,18 +346,6 @@ __device__ __forceinline__ int xcd_block_grouped(int b, int G) {
     return (i / R) * (8 * R) + x * R + (i % R);
 }
 __device__ __forceinline__ int work_block() { return xcd_block((int)blockIdx.x, (int)gridDim.x); }
-// Band variant for the fit (FARMS_FIT_XCD=band): a fit chunk's positions are
-// pooling chunks in (8x8 tile) order, x-major, so the x-th eighth of each
-// pooling chunk's positions is a band of the sensor's columns; XCD x takes that
-// eighth of every pooling chunk (bpc blocks per pooling chunk), so that its L2
-// keeps one band of the SAE across the launch and the next ones.  Bijective on
-// [0, G) when G is a multiple of bpc and bpc of 8; other grids: runs of 8.
-__device__ __forceinline__ int xcd_band_block(int b, int G, int bpc) {
-    if (bpc <= 0 || G % bpc || bpc % 8) return xcd_block_grouped(b, G);
-    const int x = b & 7, i = b >> 3, per = bpc >> 3;
-    return (i / per) * bpc + x * per + (i % per);
-}
-
 // ---------------------------------------------------------------------------
 // prep
 
@@ -1658,7 +1654,7 @@ __global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t
     __shared__ uint32_t s_tk[NPC * kFitQS];
     // (an XCD-contiguous split of a 1,024-block fit launch measured 7% slower,
     // its per-XCD work being uneven; runs of 8 blocks per XCD keep the share even)
-    const int fb = xcd_band_block(bid, G, c.fit_band);
+    const int fb = xcd_block_grouped(bid, G);
     const int w = c0 + ((fb * (int)blockDim.x + (int)threadIdx.x) >> 2);
     if (w >= c1) return;  // whole quads
     const int j = threadIdx.x & 3;
@@ -2571,6 +2567,57 @@ __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_
         : [kk] "v"(kk), [kw0] "v"(kw0), [kw1] "v"(kw1), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]),
           [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7]));
 }
+// The same fold with the member masks from the scalar unit (kSaluFold): the
+// entries' shift amounts 4 k0 are bytes of sw0:sw1 (SGPRs), entry u's members
+// are the lanes >= 4 k0, so exec = -1 << 4 k0 is one s_lshl_b64 (it reads bits
+// [5:0] of its shift operand: byte u is reached by a right shift of 8 (u % 4)).
+// The fold's only VALU instructions are then the exec-masked v_add_f64s (the
+// v_cmp per entry was about 157 of k_pool's ~1,115 VALU instructions per valid
+// event at C3, round 4).  Bitwise the fold8 sums: the same adds on the same
+// lanes.  Called with a full exec (wave-uniform control flow): the masks are
+// not intersected with it.  The shifts write SCC, hence the clobber.
+__device__ __forceinline__ void fold8_salu(double &acc, uint32_t sw0, uint32_t sw1, const double (&v)[8]) {
+    uint64_t sv;
+    uint32_t t;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n"
+        "s_lshl_b64 exec, -1, %[w0]\n"
+        "v_add_f64 %[acc], %[acc], %[v0]\n"
+        "s_lshr_b32 %[t], %[w0], 8\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v1]\n"
+        "s_lshr_b32 %[t], %[w0], 16\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v2]\n"
+        "s_lshr_b32 %[t], %[w0], 24\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v3]\n"
+        "s_lshl_b64 exec, -1, %[w1]\n"
+        "v_add_f64 %[acc], %[acc], %[v4]\n"
+        "s_lshr_b32 %[t], %[w1], 8\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v5]\n"
+        "s_lshr_b32 %[t], %[w1], 16\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v6]\n"
+        "s_lshr_b32 %[t], %[w1], 24\n"
+        "s_lshl_b64 exec, -1, %[t]\n"
+        "v_add_f64 %[acc], %[acc], %[v7]\n"
+        "s_mov_b64 exec, %[sv]\n"
+        : [acc] "+v"(acc), [sv] "=&s"(sv), [t] "=&s"(t)
+        : [w0] "s"(sw0), [w1] "s"(sw1), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]),
+          [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7])
+        : "scc");
+}
+// Fold of 8 staged entries whose packed k0 bytes (kenc: 4 k0 for the scalar
+// masks) are kw0:kw1, into this lane's sum (lane layout: kSaluFold).
+template <int K>
+__device__ __forceinline__ void fold8_k(double &acc, int kk, uint32_t kw0, uint32_t kw1, const double (&v)[8]) {
+    if constexpr (kSaluFold<K>)
+        fold8_salu(acc, __builtin_amdgcn_readfirstlane(kw0), __builtin_amdgcn_readfirstlane(kw1), v);
+    else
+        fold8(acc, kk, kw0, kw1, v);
+}
 // Row setup of a pooling window: the flattened candidate slices of rows
 // [i_lo, i_lo + nrows) (nrows <= 128), cells j in [j_lo, j_hi] of each row
 // (x-major; j already clipped to W-1 as vFlow.cpp:1000/1113 do, so for W > H a
@@ -2706,10 +2753,13 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     const uint32_t own_lin = c.serial ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
     const uint32_t own_tprev = c.serial ? (uint32_t)c.link[e].w : 0u;
     (void)ev0;
-    // lane g*K + kk: quantity g of scale kk, g = 0..3 (L, L cos, L sin, and the
-    // contributor count as a sum of 1.0: exact); lanes past 4K fold junk
-    const int grp = lane / K < 3 ? lane / K : 3;
-    const int kk = lane - grp * K;
+    // quantity g of scale kk, g = 0..3 (L, L cos, L sin, and the contributor
+    // count as a sum of 1.0: exact), on lane 4 kk + g (kSaluFold) or g K + kk;
+    // lanes past 4K fold junk.  s_k0 holds kenc(k0): 4 k0 for the scalar masks.
+    constexpr bool SF = kSaluFold<K>;
+    const int grp = SF ? (lane & 3) : (lane / K < 3 ? lane / K : 3);
+    const int kk = SF ? (lane >> 2) : lane - grp * K;
+    constexpr int kenc_mul = SF ? 4 : 1;
     constexpr int NH = kPoolHalves;  // candidates per lane per step: a step covers 64 * NH positions
 #pragma unroll
     for (int i = lane; i < kPoolSlots; i += 64) s_val[4 * i + 3] = 1.0;  // the count's "value" (staging never overwrites it)
@@ -2836,7 +2886,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 if ((pbal[h] >> lane) & 1) {
                     const int slot = cbase + (int)__popcll(pbal[h] & lt);
                     s_val[4 * slot] = pv[h][0]; s_val[4 * slot + 1] = pv[h][1]; s_val[4 * slot + 2] = pv[h][2];
-                    s_k0[slot] = (uint8_t)pk0[h];
+                    s_k0[slot] = (uint8_t)(kenc_mul * pk0[h]);
                 }
                 cbase += cntb[h];
             }
@@ -2851,7 +2901,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 double vv[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
-                fold8(acc, kk, kw0, kw1, vv);
+                fold8_k<K>(acc, kk, kw0, kw1, vv);
             }
             if (whole > 0 && staged > whole) {  // carry the rest to slots [0, staged - whole)
                 const int rest = staged - whole;
@@ -2883,7 +2933,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     if (staged > 0) {  // the last group, padded with entries in no scale (k0 = K)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (lane >= staged && lane < 8) s_k0[lane] = (uint8_t)K;
+        if (lane >= staged && lane < 8) s_k0[lane] = (uint8_t)(kenc_mul * K);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
@@ -2891,7 +2941,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         double vv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * u + grp];
-        fold8(acc, kk, kw0, kw1, vv);
+        fold8_k<K>(acc, kk, kw0, kw1, vv);
     }
     pool_finish<K>(c, e, lane, acc, total, ncon_total);
 }
@@ -2903,12 +2953,16 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 template <int K>
 __device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, double acc, int scanned, int ncon_total) {
     const int J = c.J;
-    const double cnt_kk = __shfl(acc, 3 * K + (lane < K ? lane : 0), 64);  // contributors of scale lane
+    // the lane holding quantity g of scale k (pool_one's layout)
+    auto at = [](int g, int k) { return kSaluFold<K> ? 4 * k + g : g * K + k; };
+    const int kl = lane < K ? lane : 0;
+    const double cnt_kk = __shfl(acc, at(3, kl), 64);  // contributors of scale lane
+    const double len_kk = kSaluFold<K> ? __shfl(acc, at(0, kl), 64) : acc;
     const bool is_len = lane < K;
-    const double mean = is_len && cnt_kk > 0 ? acc / cnt_kk : 0.0;
+    const double mean = is_len && cnt_kk > 0 ? len_kk / cnt_kk : 0.0;
     const double maxv = wave_max(mean);
     const int mi = maxv > 0 ? __builtin_ctzll(__ballot(is_len && mean == maxv)) : 0;
-    const double sx = __shfl(acc, K + mi, 64), sy = __shfl(acc, 2 * K + mi, 64), cnt_mi = __shfl(acc, 3 * K + mi, 64);
+    const double sx = __shfl(acc, at(1, mi), 64), sy = __shfl(acc, at(2, mi), 64), cnt_mi = __shfl(acc, at(3, mi), 64);
     if (lane == 0) {
         double gx, gy;
         int sc;
@@ -3326,13 +3380,40 @@ int mark(farms_handle *h, hipStream_t s, hipEvent_t *out) {
 
 // Read every pending bracket into h->acc (waits for their end events), then
 // the work counters; the events go back to the free list.
+// Wall time during which at least one interval runs (intervals as {start, end}).
+double union_ms(std::vector<std::pair<double, double>> &iv) {
+    std::sort(iv.begin(), iv.end());
+    double busy = 0, lo = 0, hi = 0;
+    bool open = false;
+    for (const auto &v : iv) {
+        if (open && v.first <= hi) {
+            hi = std::max(hi, v.second);
+            continue;
+        }
+        if (open) busy += hi - lo;
+        lo = v.first, hi = v.second, open = true;
+    }
+    if (open) busy += hi - lo;
+    return busy;
+}
+
 int harvest(farms_handle *h) {
     std::vector<hipEvent_t> used;
     used.reserve(2 * h->brk.size());
+    // the kernel brackets on the device timeline (ms after the first bracket's
+    // start, negative if before): their union is the wall time during which a
+    // fit (pooling) launch runs, whatever the streams overlap -- the sum of the
+    // brackets counts overlapping launches of two fit streams twice
+    std::vector<std::pair<double, double>> iv_fit, iv_pool;
     for (const auto &b : h->brk) {
         HIPCHK(hipEventSynchronize(b.b));
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, b.a, b.b));
+        if (b.kind == kBrFitKernel || b.kind == kBrPoolKernel) {
+            float t0 = 0;
+            HIPCHK(hipEventElapsedTime(&t0, h->brk.front().a, b.a));
+            (b.kind == kBrFitKernel ? iv_fit : iv_pool).emplace_back((double)t0, (double)t0 + (double)ms);
+        }
         switch (b.kind) {
         case kBrPrep: h->acc.ms_prep += ms; break;
         case kBrFitSweep: h->acc.ms_fit += ms; break;
@@ -3343,6 +3424,8 @@ int harvest(farms_handle *h) {
         used.push_back(b.a);
         used.push_back(b.b);
     }
+    h->acc.ms_fit_busy += union_ms(iv_fit);
+    h->acc.ms_pool_busy += union_ms(iv_pool);
     h->brk.clear();
     std::sort(used.begin(), used.end());
     used.erase(std::unique(used.begin(), used.end()), used.end());
@@ -3554,11 +3637,6 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.hdr_ring = h->hdr_ring; c.val_ring = h->val_ring;
     c.nwords = h->nwords; c.NB = h->NB; c.C2 = h->pool_chunk;
     c.ring0 = (int)(h->chunk_base % h->NB);
-    {  // FARMS_FIT_XCD=band: the fit's blocks by sensor band per XCD (xcd_band_block)
-        const char *fx = getenv("FARMS_FIT_XCD");
-        const int bpc = h->pool_chunk / kFitQS;
-        c.fit_band = fx && fx[0] == 'b' && h->pool_chunk % kFitQS == 0 ? bpc : 0;
-    }
     const int span = 2 * h->M + 1;  // pooling window rows and columns
     c.pool_bw = (span * span + 63) / 64 + 1;  // flattened window positions (+1: a two-half step reads a word ahead)
     c.pool_rs = span;                     // <= 2 segments per window row, 4 B each
@@ -4107,28 +4185,9 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // 113 instead of 97 ms at C3).
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    // FARMS_POOL_CU_SKIP = k (0..8, A/B aid): k CUs of every 32 left out of
-    // the pooling stream's CU mask, so that the fit chain always finds free
-    // slots there.  Word j of the mask clears bits 8 (t % 4) + (j + t) % 8, t <
-    // k: k per 32-CU word and k per residue mod 8, whichever way the bits map
-    // to the XCDs.
-    std::vector<uint32_t> pool_mask;
-    if (const char *v = getenv("FARMS_POOL_CU_SKIP")) {
-        const int k = std::max(0, std::min(atoi(v), 8));
-        int dev = 0;
-        hipDeviceProp_t dp{};
-        if (k > 0 && hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&dp, dev) == hipSuccess &&
-            dp.multiProcessorCount % 32 == 0) {
-            pool_mask.assign((size_t)dp.multiProcessorCount / 32, 0xffffffffu);
-            for (int j = 0; j < (int)pool_mask.size(); ++j)
-                for (int t = 0; t < k; ++t) pool_mask[j] &= ~(1u << (8 * (t & 3) + ((j + t) & 7)));
-        }
-    }
     if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        (pool_mask.empty()
-             ? hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo)
-             : hipExtStreamCreateWithCUMask(&h->s_pool, (uint32_t)pool_mask.size(), pool_mask.data())) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_copy, hipStreamNonBlocking, prio_hi) != hipSuccess)  // (device calls: odd fits)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {

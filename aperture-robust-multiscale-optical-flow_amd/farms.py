@@ -83,6 +83,8 @@ class FarmsStats(ctypes.Structure):
         ("pool_candidates", ctypes.c_double),
         ("pool_contributors", ctypes.c_double),
         ("n_owned", ctypes.c_int64),
+        ("ms_fit_busy", ctypes.c_double),
+        ("ms_pool_busy", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

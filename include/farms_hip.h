@@ -103,6 +103,11 @@ typedef struct {
     double pool_candidates;   /* sum over valid events of candidate cells scanned */
     double pool_contributors; /* sum over valid events of contributing cells (largest scale) */
     int64_t n_owned;          /* events in the owned columns (all of them unless own_x1 is set) */
+    /* wall time during which at least one k_fit (k_pool) launch runs: the union
+     * of the launch brackets on the device timeline.  Equal to ms_fit_kernel
+     * when the launches never overlap; below it when two fit streams run
+     * launches side by side (fs 7), where the sum counts the overlap twice. */
+    double ms_fit_busy, ms_pool_busy;
 } farms_stats;
 
 /* vFlowManager ctor defaults: 320 x 320, filter 3, 5 inliers (main.cpp:21-24),
@@ -206,8 +211,9 @@ int farms_num_scales(const farms_handle *h);
 
 /* The kernels the handle's next call runs (its filter and scales, and the
  * FARMS_FIT_* / FARMS_POOL_* tuning knobs as they are now), and the candidate
- * build the last pooling call took (decided on the device per call; waits for
- * it), as a JSON object in buf (NUL-terminated, truncated to len):
+ * build of the last pooling call enqueued (the host decides it when it
+ * enqueues the call, from the prep's kill-window reach; this function does not
+ * synchronise), as a JSON object in buf (NUL-terminated, truncated to len):
  * {"fit": "k_fit_quad<2>", "fit_mode": 1, "pool": "k_pool<11>", "pool_cap": 7,
  * "cand_last": "k_cand"}.  Not in the reference (measurement aid for bench.py). */
 int farms_kernel_info(const farms_handle *h, char *buf, int32_t len);

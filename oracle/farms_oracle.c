@@ -30,6 +30,7 @@
 struct farms_oracle {
     int W, H;
     int serial; /* vFlowManager::run semantics (farms_oracle.h) */
+    int eigen;  /* 34 (default) or 33: the Eigen version whose GEMV order (A2*At)*Y follows (farms_oracle_set_eigen) */
     /* libm of the path: glibc's atan2 / sin / cos (the reference's) unless a
      * test swaps in another implementation (farms_oracle_set_libm) */
     double (*f_atan2)(double, double);
@@ -45,7 +46,7 @@ struct farms_oracle {
     double *flow_theta; /* flowSurfaceThetaOn/Of */
     /* computeTrueFlow scratch (vFlow.cpp:966-977) */
     double *pool, *pool_x, *pool_y;
-    double *scratch; /* computeGrads A/Y rows: 4 * planeSize doubles */
+    double *scratch; /* computeGrads A/Y rows and one row's products: 5 * planeSize doubles */
 };
 
 int farms_oracle_create(int width, int height, int filter_size, int min_inliers,
@@ -69,6 +70,7 @@ int farms_oracle_create(int width, int height, int filter_size, int min_inliers,
     o->window_jump = window_jump;
     o->max_window = max_window;
     o->nscales = nscales;
+    o->eigen = 34;
     o->f_atan2 = atan2;
     o->f_sin = sin;
     o->f_cos = cos;
@@ -82,7 +84,7 @@ int farms_oracle_create(int width, int height, int filter_size, int min_inliers,
     o->pool = (double *)calloc((size_t)nscales, sizeof(double));
     o->pool_x = (double *)calloc((size_t)nscales, sizeof(double));
     o->pool_y = (double *)calloc((size_t)nscales, sizeof(double));
-    o->scratch = (double *)calloc(4 * (size_t)o->plane_size, sizeof(double));
+    o->scratch = (double *)calloc(5 * (size_t)o->plane_size, sizeof(double));
     if (!o->scratch || !o->cs_x || !o->cs_y || !o->cs_t || !o->last_time || !o->flow_len || !o->flow_theta ||
         !o->pool || !o->pool_x || !o->pool_y) {
         farms_oracle_destroy(o);
@@ -153,6 +155,36 @@ static double eigen_det3_partialpivlu(const double ata[9])
     return (transpositions & 1) ? -prod : prod;
 }
 
+/* Eigen 3.3's column-major GEMV (GeneralMatrixVector.h, as published in the
+ * 3.3 series; the 3.4 rewrite accumulates every row sequentially from zero) for
+ * temp = (A2*At) * Y, the 3 x n temporary times the n x 1 runtime vector Y
+ * (vFlow.cpp:1338), with SSE2 packets of 2 doubles, for one of the two packet
+ * rows (rows 0 and 1: a and b; row 2, the intercept c, is a scalar remainder
+ * row and is never used by the reference).  The destination starts at zero
+ * (dst.setZero()) and is 16-B aligned, so rows 0-1 form the one aligned packet;
+ * the temporary's column stride is 3 (odd), so alignmentStep = 1 and the
+ * kernel's offset1 / offset3 swap (its `FirstAligned && alignmentStep==1` test
+ * reads the enum constant): each block of 4 columns i..i+3 takes lhs0..lhs3 =
+ * columns i, i+3, i+2, i+1 and _EIGEN_ACCUMULATE_PACKETS adds
+ *     res = res + ((p[i] + p[i+3]) + (p[i+2] + p[i+1]));
+ * the n % 4 remaining columns follow one at a time (res = res + p[k]).  p[k] is
+ * (A2*At)(r, k) * Y(k) (alpha = 1: exact).  Only the order of the additions
+ * differs from 3.4; whether it changes a record is measured, not assumed
+ * (tools/eigen_sensitivity.py). */
+static double eigen33_gemv_packet_row(const double *p, int n)
+{
+    double res = 0.0;
+    const int bound = n / 4 * 4;
+    for (int i = 0; i < bound; i += 4) res = res + ((p[i] + p[i + 3]) + (p[i + 2] + p[i + 1]));
+    for (int k = bound; k < n; ++k) res = res + p[k];
+    return res;
+}
+
+void farms_oracle_set_eigen(farms_oracle *o, int version)
+{
+    if (o) o->eigen = version == 33 ? 33 : 34;
+}
+
 /* ---- computeGrads (vFlow.cpp:1214-1381) ------------------------------------- */
 
 /* n rows: X[k], Y[k] (stored event coords), T[k] (stored stamp, double).
@@ -160,7 +192,7 @@ static double eigen_det3_partialpivlu(const double ata[9])
  * DET >= 1 (vFlow.cpp:1323 returns before touching them otherwise). */
 static int compute_grads(const farms_oracle *o, int n, const double *X, const double *Y, const double *T,
                          double cen_x, double cen_y, double cen_t, double *dtdy, double *dtdx,
-                         double *Yt /* scratch n */)
+                         double *Yt /* scratch 2n */)
 {
     /* A (n x 3) rows (X, Y, 1); Y = t*1e-6, or (t - 2^32)*1e-6 for stamps in the
      * future of the event (vFlow.cpp:1224-1234). */
@@ -206,16 +238,23 @@ static int compute_grads(const farms_oracle *o, int n, const double *X, const do
     double abc[3];
     for (int r = 0; r < 3; ++r) {
         const double a0 = d[0 * 3 + r], a1 = d[1 * 3 + r], a2 = d[2 * 3 + r];
-        double acc = 0.0;
+        double *pr = Yt + n; /* scratch: the n products of row r, (A2*At)(r,k) * Y(k) */
         for (int k = 0; k < n; ++k) {
             double m;
             if (gemm) m = ((((0.0 + a0 * X[k]) + a1 * Y[k]) + a2 * 1.0)) + 0.0;
             else m = (a0 * X[k] + a1 * Y[k]) + a2 * 1.0;
-            double pr = m * Yt[k];
-            if (!gemv && k == 0) acc = pr;
-            else acc = acc + pr;
+            pr[k] = m * Yt[k];
         }
-        abc[r] = gemv ? acc + 0.0 : acc;
+        if (gemv && o->eigen == 33 && r < 2)
+            abc[r] = eigen33_gemv_packet_row(pr, n);
+        else {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) {
+                if (!gemv && k == 0) acc = pr[k];
+                else acc = acc + pr[k];
+            }
+            abc[r] = gemv ? acc + 0.0 : acc;
+        }
     }
 
     /* vFlow.cpp:1349-1377 */

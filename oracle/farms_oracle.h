@@ -83,6 +83,14 @@ int farms_oracle_pool_given(farms_oracle *o, const int32_t *x, const int32_t *y,
 void farms_oracle_set_libm(farms_oracle *o, double (*f_atan2)(double, double), double (*f_sin)(double),
                            double (*f_cos)(double));
 
+/* The Eigen version whose evaluation order temp = A2*At*Y (vFlow.cpp:1338)
+ * follows: 34 (default; the 3.4 GEMV sums every row sequentially from zero) or
+ * 33 (the 3.3 GEMV adds each block of 4 columns as a packet tree,
+ * res + ((p0 + p3) + (p2 + p1)), on the rows of a and b).  The reference pins no
+ * Eigen version (CMakeLists.txt:19, README.md:19); this switch measures how much
+ * the choice moves the records.  Other values mean 34. */
+void farms_oracle_set_eigen(farms_oracle *o, int version);
+
 /* Number of pooling scales (floor(maxWindow/windowJump) + 1). */
 int farms_oracle_num_scales(const farms_oracle *o);
 

@@ -43,6 +43,8 @@ def load() -> ctypes.CDLL:
         lib.farms_oracle_serial_first.restype = None
         lib.farms_oracle_set_libm.argtypes = [ctypes.c_void_p] * 4
         lib.farms_oracle_set_libm.restype = None
+        lib.farms_oracle_set_eigen.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.farms_oracle_set_eigen.restype = None
         lib.farms_oracle_pool_given.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int64] + [ctypes.c_void_p] * 3
         _lib = lib
     return _lib
@@ -64,7 +66,7 @@ class OracleFlow:
     """CPU vFlowManager batch loop: OracleFlow(height, width, filter_size, min_evts)."""
 
     def __init__(self, height=320, width=320, filter_size=3, min_evts_on_plane=5, window_jump=5, max_window=50,
-                 serial=False, libm="glibc"):
+                 serial=False, libm="glibc", eigen=34):
         self._lib = load()
         h = ctypes.c_void_p()
         rc = self._lib.farms_oracle_create(int(width), int(height), int(filter_size), int(min_evts_on_plane),
@@ -74,6 +76,11 @@ class OracleFlow:
         self._h = h
         if serial:
             self._lib.farms_oracle_set_serial(self._h, 1)
+        if eigen not in (33, 34):
+            raise ValueError("eigen must be 34 (default) or 33")
+        # the evaluation order of A2*At*Y (vFlow.cpp:1338): Eigen 3.4's, or 3.3's
+        # packet-tree GEMV (farms_oracle_set_eigen)
+        self._lib.farms_oracle_set_eigen(self._h, int(eigen))
         if libm == "cr":
             # the HIP path's correctly rounded atan2 / sin / cos (host build of
             # csrc/farms_libm.h): checks the rest of the GPU arithmetic bitwise

@@ -101,3 +101,23 @@ def test_rooflines_name_the_dominant_kernel_per_config():
             assert r["frac"] == round(r["traffic"] / (r["avg_launch_us"] * 1e-6) / 1e9 / 8000.0, 4)
         else:
             assert r["frac"] is None
+
+
+def test_rooflines_use_busy_wall_time_for_overlapping_launches():
+    """With two fit streams the launch brackets overlap: the roofline's launch
+    duration is the busy wall time (union of the brackets, farms_stats
+    ms_*_busy) per launch, so launches x duration stays within the step; the
+    bracket sum is reported beside it (round-4 review: C4 summed 93.7 ms of fit
+    brackets in a 61.4 ms step)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ts = {"fit_launches": 763, "pool_launches": 48, "ms_fit_kernel": 93.7, "ms_pool_kernel": 55.0,
+          "ms_fit_busy": 56.6, "ms_pool_busy": 55.0}
+    cs = {"n_events": 1000, "n_owned": 1000, "n_valid": 400, "sae_cells": 169e3, "pool_cells": 4e6}
+    rl = bench.rooflines(4, "segments", ts, cs, {"fit": "k_fit_quad<3>", "pool": "k_pool<11>"})
+    f = rl["k_fit"]
+    assert f["avg_launch_us"] == round(56.6e3 / 763, 2)
+    assert f["ms_busy_per_step"] == 56.6 and f["ms_bracket_sum_per_step"] == 93.7
+    assert rl["dominant"] == "k_fit"
+    assert f["launches_per_step"] * f["avg_launch_us"] / 1e3 <= 61.4

@@ -564,3 +564,82 @@ def test_work_order_builds_are_bitwise_identical(monkeypatch):
                 outs.append(fm.process(x, y, t, p))
     for o in outs[1:]:
         assert bitwise_equal(outs[0], o)
+
+
+@pytest.mark.parametrize("shift", ["2", "4"])
+def test_work_order_tile_sizes_are_bitwise_identical(shift, monkeypatch):
+    """FARMS_TILE_SHIFT (log2 of the work-order tile's edge: 4x4 and 16x16
+    tiles against the default 8x8) changes the order in which the fit and the
+    pooling visit a chunk's events, the column bands of k_cand and the block
+    placement, never the records (both order paths: k_chunk_order and the
+    device-wide sort)."""
+    ev = farms.synth_config(3, 150_000)
+    x, y, t, p = ev.relative()
+    monkeypatch.delenv("FARMS_TILE_SHIFT", raising=False)
+    with farms.FlowManager(720, 1280, 5, 5) as fm:
+        ref = fm.process(x, y, t, p)
+    monkeypatch.setenv("FARMS_TILE_SHIFT", shift)
+    for order in ("", "sort"):
+        if order:
+            monkeypatch.setenv("FARMS_ORDER", order)
+        else:
+            monkeypatch.delenv("FARMS_ORDER", raising=False)
+        with farms.FlowManager(720, 1280, 5, 5) as fm:
+            assert bitwise_equal(ref, fm.process(x, y, t, p)), (shift, order)
+
+
+def _device_run(fm, x, y, t, p, splits, two_phase):
+    """Records of one device-resident run: process_device per split, or the
+    two-phase calls with the fit of split b+1 issued before the pooling of b
+    (two fits pending, as multirank.Stepper runs the x-strips)."""
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x, y, t.view(np.int32), p)]
+    n = len(x)
+    o = {c: torch.zeros(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+         for c in farms.COLUMNS[4:]}
+
+    def sl(a, b):
+        return [v[a:b] for v in d], {c: v[a:b] for c, v in o.items()}
+
+    if not two_phase:
+        for a, b in splits:
+            ins, out = sl(a, b)
+            fm.process_device(*ins, out)
+    else:
+        pending = 0
+        for a, b in splits:
+            ins, out = sl(a, b)
+            fm.fit_device(*ins, out)
+            pending += 1
+            if pending == 2:
+                fm.pool_device()
+                pending -= 1
+        for _ in range(pending):
+            fm.pool_device()
+    torch.cuda.synchronize()
+    g = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
+    g.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
+    return g
+
+
+@pytest.mark.parametrize("fs", [5, 7])
+def test_fit_streams_on_device_paths_are_bitwise_identical(fs, monkeypatch):
+    """The fit sweep on one stream or two (FARMS_FIT_STREAMS; even / odd fit
+    chunks, the fs-7 default of the device calls): independent even / odd SAE
+    preps, final commits waiting across streams and a k_flow waiting on the
+    other stream's last fit.  Run where the two streams are used -- device
+    calls (farms_process_device, split in several calls) and the two-phase
+    calls with two fits pending (farms_fit_device / farms_pool_device, the
+    x-strips' pipelined step) -- with small fit chunks (many of each parity):
+    bitwise the host path's one-stream run (farms_process)."""
+    ev = farms.synth_config(4 if fs == 7 else 3, 200_000)
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(720, 1280, fs, 5) as fm:
+        ref = fm.process(x, y, t, p)
+    splits = [(0, 70_001), (70_001, 70_002), (70_002, 140_000), (140_000, len(x))]
+    for streams in ("1", "2"):
+        monkeypatch.setenv("FARMS_FIT_STREAMS", streams)
+        for two_phase in (False, True):
+            with farms.FlowManager(720, 1280, fs, 5, fit_chunk=8192) as fm:
+                g = _device_run(fm, x, y, t, p, splits, two_phase)
+            assert bitwise_equal(ref, g), (streams, two_phase, compare(ref, g))

@@ -185,6 +185,25 @@ constexpr int kPoolMaxM = 63;  // largest maxWindow (2M+1 rows <= 2 x 64 lanes; 
 template <int K>
 constexpr bool kSaluFold = FARMS_POOL_SALU && 4 * K < 64;
 
+// Diagnostic builds (make variant NAME=stamps DEFS=-DFARMS_POOL_STAMPS): k_pool
+// reads the shader clock at its phase boundaries and adds each valid event's
+// cycles per phase into g_pool_stamps (farms_debug_pool_stamps reads and
+// clears them): [0] prologue (descriptor), [1] row setup, [2] candidate pass
+// (fold included), [3] fold, [4] finish, [5] valid events, [6] steps, [7] fold
+// groups.  The clock reads wait on the LDS counter too: a few % slower.
+#ifdef FARMS_POOL_STAMPS
+// per-wave sums in registers (pool_st), added by lane 0 at the wave's end into
+// one of 1,024 slot rows (block % 1024: no contention on one address)
+constexpr int kStampRows = 1024;
+__device__ unsigned long long g_pool_stamps[8 * kStampRows];
+struct PoolSt { uint64_t v[8]; };
+#define POOL_CLOCK(v) const uint64_t v = (uint64_t)clock64()
+#define POOL_STAMP_ADD(i, x) (pool_st.v[i] += (uint64_t)(x))
+#else
+#define POOL_CLOCK(v)
+#define POOL_STAMP_ADD(i, x)
+#endif
+
 struct Ctx {
     int W, H, n;
     int64_t WH;            // cells stored by this handle (region columns x H)
@@ -305,6 +324,16 @@ __device__ __forceinline__ int64_t sae_resolve_head(uint3 h, int e, bool &defer)
         }
     }
     return (h.z & kHeadVisited) ? (int64_t)h.x : int64_t(-1);
+}
+// The same resolution in 32 bits (fit_event_quad_u): the stamp (0 for a
+// never-visited cell, the reference's Event(0,0,0,0)), whether the cell is
+// visited, and whether its tail decides (then the stamp is the provisional t1).
+__device__ __forceinline__ uint32_t sae_head_stamp(uint3 h, int e, bool &vis, bool &defer) {
+    const bool now = (int)h.z < 0 && (int)(h.z & kHeadE1Mask) <= e;  // touched, first in-chunk event <= e
+    defer = now && (h.z & kHeadMore) != 0;
+    const bool snap = (h.z & kHeadVisited) != 0;
+    vis = now || snap;
+    return now ? h.y : (snap ? h.x : 0u);
 }
 // The stamp as of e of a deferred cell q (its head says: touched, first event
 // at or before e, more than one in-chunk event; t1 its first stamp), from the
@@ -1233,6 +1262,7 @@ __device__ __forceinline__ void fit_event_quad(const Ctx &c, int4 fd, uint32_t s
 template <int FR>
 __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t seq, int j, uint32_t *ut, double &vx_out,
                                                  double &vy_out, bool &acc_out) {
+    (void)seq;
     constexpr int side = 2 * FR + 1, np = side * side, US = 4 * FR + 1;
     const int W = c.W, H = c.H;
     const int e = fd.x, ex = fd.y, ey = fd.z;  // the fit descriptor (k_fit_desc)
@@ -1251,45 +1281,43 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
         any |= wok[w];
     }
     if (!any) return;  // uniform over the quad
-    auto load_col = [&](int u0, int v0, int len, uint3 *col) {
-        const bool inr = u0 >= 0 && u0 < W && u0 >= c.X0 && u0 < c.XR1;  // outside the stored region: never visited
-        const int cbase = (u0 - c.X0) * H + v0;
-#pragma unroll
-        for (int i = 0; i < len; ++i) {
-            const int v = v0 + i;
-            // unconditional load from a clamped index, then select: a load under a
-            // branch is waited for at the branch's end, serializing the column
-            const bool ok = inr && v >= 0 && v < H;
-            const uint3 hd = sae_head(c, ok ? (uint32_t)(cbase + i) : 0u);
-            col[i] = ok ? hd : make_uint3(0, 0, 0);
-        }
-    };
-    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union columns
+    // ---- window scores (vFlow.cpp:870-912), exact int64: this lane's union
+    // columns.  A cell outside the stored region reads the buffer's guard head
+    // (index WH: zero, never written), which resolves to "never visited", as
+    // the reference's Event(0,0,0,0) cells do; cells outside the sensor also
+    // read it and only enter the scores of windows the clip rejects (wok) and
+    // union slots no accepted window reads, so they need no test of their own.
     uint64_t umask = 0;  // visited bits of this lane's union cells: (slot * US + row), slot = column / 4
-    uint64_t pend = 0;   // cells whose tail decides (sae_resolve_head): fixed after the scan
+    uint64_t pend = 0;   // cells whose tail decides (sae_head_stamp): fixed after the scan
     constexpr int NC = (US + 3) / 4;  // union columns per lane (the last one absent on some lanes)
-    auto ddiff = [&](uint32_t tk) { return (int64_t)te - (int64_t)tk + (tk > te ? (int64_t(1) << 32) : 0); };
+    // t_e - t_k + [t_k > t_e] 2^32 (vFlow.cpp:891-905) is the 32-bit wrapped
+    // difference, zero-extended: both lie in [0, 2^32) and agree mod 2^32
+    auto ddiff = [&](uint32_t tk) { return (int64_t)(uint32_t)(te - tk); };
+    const uint32_t guard = (uint32_t)c.WH;
 #pragma unroll
     for (int sl = 0; sl < NC; ++sl) {  // unrolled: the loads of every column are in flight together
         const int du = -2 * FR + j + 4 * sl;
         if (du > 2 * FR) continue;
+        const int u0 = ex + du, v0 = ey - 2 * FR;
+        const bool inr = u0 >= c.X0 && u0 < c.XR1;  // (the stored region lies inside the sensor)
+        const int cbase = (u0 - c.X0) * H + v0;
         uint3 col[US];
-        load_col(ex + du, ey - 2 * FR, US, col);
-        const int u = ex + du;
-        if (u < 0 || u >= W) continue;
+#pragma unroll
+        for (int i = 0; i < US; ++i) {
+            // unconditional loads (a load under a branch is waited for at the
+            // branch's end, serializing the column)
+            const bool ok = inr && v0 + i >= 0 && v0 + i < H;
+            col[i] = sae_head(c, ok ? (uint32_t)(cbase + i) : guard);
+        }
         const int ucol = du + 2 * FR;  // union column index
         int64_t dd[US];
 #pragma unroll
         for (int i = 0; i < US; ++i) {
-            const int v = ey + i - 2 * FR;
-            dd[i] = 0;
-            if (v < 0 || v >= H) continue;
-            bool defer;
-            const int64_t st = sae_resolve_head(col[i], e, defer);
-            const uint32_t tk = st < 0 ? 0u : (uint32_t)st;
+            bool vis, defer;
+            const uint32_t tk = sae_head_stamp(col[i], e, vis, defer);
             ut[(ucol * US + i) * kFitQS] = tk;
-            umask |= st >= 0 ? 1ull << ((ucol >> 2) * US + i) : 0ull;
-            pend |= defer ? 1ull << ((ucol >> 2) * US + i) : 0ull;
+            umask |= vis ? 1ull << (sl * US + i) : 0ull;
+            pend |= defer ? 1ull << (sl * US + i) : 0ull;
             dd[i] = ddiff(tk);
         }
 #pragma unroll
@@ -1364,18 +1392,23 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     // the union stamps were written by the other lanes of this wave's quad
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    auto cell = [&](int k, int64_t &X, int64_t &Y, uint32_t &T) {
+    auto cell = [&](int k, uint32_t &X, uint32_t &Y, uint32_t &T) {
         const int kx = k / side, ky = k % side;
-        const int cx = bi + kx - FR, cy = bj + ky - FR;
-        const bool vk = (vis >> k) & 1;
-        X = vk ? cx : 0; Y = vk ? cy : 0; T = ut[((ub + kx) * US + vb + ky) * kFitQS];
+        const bool vk = (vis >> k) & 1;  // never-visited cells store (0, 0): vFlow.cpp:1226-1233
+        X = vk ? (uint32_t)(bi + kx - FR) : 0u; Y = vk ? (uint32_t)(bj + ky - FR) : 0u;
+        T = ut[((ub + kx) * US + vb + ky) * kFitQS];
     };
-    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;  // exact: any split and order
+    // Y (vFlow.cpp:1229-1233); (t - 2^32) is exact in double, so selecting
+    // before the one multiply is the reference's expression
+    auto ytime = [&](uint32_t T) { return (T > te ? (double)T - kMaxStamp : (double)T) * kTsToSec; };
+    // AtA (vFlow.cpp:1307-1311): integer sums, exact in any split and order
+    // (coordinates < 2^16: the 24-bit products are exact)
+    int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
 #pragma unroll 1
     for (int k = j; k < np; k += 4) {
-        int64_t X, Y; uint32_t T;
+        uint32_t X, Y, T;
         cell(k, X, Y, T);
-        sxx += X * X; sxy += X * Y; sx += X; syy += Y * Y; sy += Y;
+        sxx += __umul24(X, X); sxy += __umul24(X, Y); sx += X; syy += __umul24(Y, Y); sy += Y;
     }
     sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
     syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
@@ -1402,10 +1435,9 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
 #pragma unroll 1
     for (int kb = 0; kb < np; kb += 4) {
         const int k = kb + j < np ? kb + j : np - 1;
-        int64_t Xi, Yi; uint32_t T;
+        uint32_t Xi, Yi, T;
         cell(k, Xi, Yi, T);
-        const double X = (double)Xi, Y = (double)Yi, Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double X = (double)Xi, Y = (double)Yi, yt = ytime(T);
         double m0, m1;
         if (gemm) {
             m0 = (((0.0 + d0 * X) + d3 * Y) + d6 * 1.0) + 0.0;
@@ -1424,22 +1456,21 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     }
     if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
     const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
+    const double half = dtdp / 2;
     const double ccx = (double)ex, ccy = (double)ey;
     int inliers = 0;
 #pragma unroll 1
     for (int k = j; k < np; k += 4) {
-        int64_t Xi, Yi; uint32_t T;
+        uint32_t Xi, Yi, T;
         cell(k, Xi, Yi, T);
-        const double Tk = (double)T;
-        const double yt = T > te ? (Tk - kMaxStamp) * kTsToSec : Tk * kTsToSec;
+        const double yt = ytime(T);
         const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
         const double actualdt = yt - cz;
-        if (fabs(planedt - actualdt) < dtdp / 2 && yt > 0) ++inliers;
+        if (fabs(planedt - actualdt) < half && yt > 0) ++inliers;
     }
     inliers += xch32<0>(inliers);
     inliers += xch32<1>(inliers);
     if (inliers < c.min_inl) return;  // vFlow.cpp:934-942
-    (void)dtdp;
     vx_out = r0;  // the plane's slopes: k_flow turns them into (Vx, Vy) (vFlow.cpp:1373-1377)
     vy_out = r1;
     acc_out = true;
@@ -1638,8 +1669,13 @@ __device__ __forceinline__ void fit_event_quad_r(const Ctx &c, int4 fd, uint32_t
 // Four lanes per event of chunk [c0, c1) in tile order; lane 0 of the quad stores.
 // (MODE 0: re-gather the winning window; 1: union tile, columns per lane;
 // 2: union tile, rows per lane)
+// Occupancy floor of the quad fit: fs <= 5 fits keep 7 waves per SIMD (at
+// most 72 VGPRs; their 5.2-KB LDS tile allows 7.5); the fs-7 fit is held to
+// 3.75 waves per SIMD by its 10.8-KB tile anyway, so it may use 128 VGPRs.
+template <int FR>
+constexpr int kFitMinWaves = FR <= 2 ? 7 : 1;
 template <int FR, int MODE>
-__global__ __launch_bounds__(64) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
+__global__ __launch_bounds__(64, kFitMinWaves<FR>) void k_fit_quad(Ctx c, int c0, int c1, uint32_t seq, FitPrep pr) {
     const int G = (int)gridDim.x - pr.blocks;  // the fit's blocks
     if ((int)blockIdx.x >= G) {
         fit_prep_thread(c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq,
@@ -2739,10 +2775,17 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
 // 64 staged entries (contributors first, in rank order).
 template <int K>
 __device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, double acc, int scanned, int ncon_total);
+#ifdef FARMS_POOL_STAMPS
+#define POOL_ST_PARAM , PoolSt &pool_st
+#define POOL_ST_ARG , pool_st
+#else
+#define POOL_ST_PARAM
+#define POOL_ST_ARG
+#endif
 template <int K>
 __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
                                          int row_i0, int total, int ev0, const uint64_t *s_start,
-                                         const uint32_t *s_row, double *s_val, uint8_t *s_k0) {
+                                         const uint32_t *s_row, double *s_val, uint8_t *s_k0 POOL_ST_PARAM) {
     static_assert(4 * K <= 64, "one lane per (quantity, scale)");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
@@ -2802,6 +2845,9 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 #pragma unroll
     for (int h = 0; h < NH; ++h) { pbal[h] = 0; pv[h][0] = pv[h][1] = pv[h][2] = 0.0; pk0[h] = K; }
     int staged = 0;  // (wave-uniform) staged entries not yet folded, at slots [0, staged)
+#ifdef FARMS_POOL_STAMPS
+    uint64_t st_fold = 0, st_steps = 0, st_groups = 0;
+#endif
     for (int f0 = 0;; f0 += 64 * NH) {
         const bool have = f0 < total;  // wave-uniform
         bool con[NH];
@@ -2895,6 +2941,14 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
             __builtin_amdgcn_wave_barrier();
             const int whole = staged & ~7;
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+#ifdef FARMS_POOL_STAMPS
+            POOL_CLOCK(tf0);
+            st_groups += whole >> 3;
+            st_steps += 1;
+#endif
+            // (each group waits for its own LDS reads: reading group r + 8
+            // while group r is added, in two register sets, measured slower,
+            // C3 80.7 against 77.4 ms, profiles/r05_ab_fold_prefetch.log)
 #pragma unroll 1
             for (int r = 0; r < whole; r += 8) {
                 const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
@@ -2903,6 +2957,12 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
                 for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * (r + u) + grp];
                 fold8_k<K>(acc, kk, kw0, kw1, vv);
             }
+#ifdef FARMS_POOL_STAMPS
+            {
+                POOL_CLOCK(tf1);
+                st_fold += tf1 - tf0;
+            }
+#endif
             if (whole > 0 && staged > whole) {  // carry the rest to slots [0, staged - whole)
                 const int rest = staged - whole;
                 double m0 = 0.0, m1 = 0.0, m2 = 0.0;
@@ -2943,7 +3003,17 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
         for (int u = 0; u < 8; ++u) vv[u] = s_val[4 * u + grp];
         fold8_k<K>(acc, kk, kw0, kw1, vv);
     }
+#ifdef FARMS_POOL_STAMPS
+    POOL_STAMP_ADD(3, st_fold);
+    POOL_STAMP_ADD(6, st_steps);
+    POOL_STAMP_ADD(7, st_groups);
+    POOL_CLOCK(tp0);
+#endif
     pool_finish<K>(c, e, lane, acc, total, ncon_total);
+#ifdef FARMS_POOL_STAMPS
+    POOL_CLOCK(tp1);
+    POOL_STAMP_ADD(4, tp1 - tp0);
+#endif
 }
 
 // Every per-scale sum of event e folded (lane g * K + kk holds quantity g of
@@ -2985,12 +3055,17 @@ __device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, doubl
 template <int K>
 __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, uint32_t teu, int buf, int lane,
                                            int ev0, uint64_t *s_start, uint32_t *s_row, double *s_val,
-                                           uint8_t *s_k0) {
+                                           uint8_t *s_k0 POOL_ST_PARAM) {
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
+    POOL_CLOCK(tr0);
     const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
-    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0);
+    POOL_CLOCK(tr1);
+    POOL_STAMP_ADD(1, tr1 - tr0);
+    pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0 POOL_ST_ARG);
+    POOL_CLOCK(tr2);
+    POOL_STAMP_ADD(2, tr2 - tr1);
 }
 
 // One wavefront (= one workgroup, so that a finished event frees its slot at
@@ -3021,15 +3096,30 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
     uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + nbw);
     double *s_val = reinterpret_cast<double *>(s_start + nbw + nrs);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * kPoolSlots);
+    POOL_CLOCK(tk0);
     const int w = c0 + work_block();
     if (w >= c1) return;
     // the event and its fields in one 16-B load (k_pool_desc)
     const int4 d = c.qe[w];
     if (d.x < 0) return;  // invalid flow, or a halo event (pooled by its owner)
+#ifdef FARMS_POOL_STAMPS
+    PoolSt pool_st = {};
+    {
+        POOL_CLOCK(tk1);
+        POOL_STAMP_ADD(0, tk1 - tk0);
+        POOL_STAMP_ADD(5, 1);
+    }
+#endif
     const int e = d.x, ex = d.y, ey = d.z;
     const uint32_t teu = (uint32_t)d.w;
     const int buf = (c.ring0 + w / c.C2) % c.NB;  // the event's chunk's candidate buffer
-    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0);
+    pool_event<K>(c, e, ex, ey, teu, buf, lane, (w / c.C2) * c.C2, s_start, s_row, s_val, s_k0 POOL_ST_ARG);
+#ifdef FARMS_POOL_STAMPS
+    if (lane == 0) {
+        unsigned long long *row = g_pool_stamps + 8 * (blockIdx.x % kStampRows);
+        for (int i = 0; i < 8; ++i) atomicAdd(&row[i], (unsigned long long)pool_st.v[i]);
+    }
+#endif
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -3110,8 +3200,8 @@ __global__ void k_seed_sae(Ctx c, const int64_t *stamp) {
     SaeHead hd{};
     hd.w = s >= 0 ? kHeadVisited : 0u;  // not touched
     hd.tsnap = s >= 0 ? (uint32_t)s : 0u;
-    c.cells.head[q] = hd;  // both SAE buffers (heads are contiguous: buffer 1 follows buffer 0)
-    c.cells.head[q + c.WH] = hd;
+    c.cells.head[q] = hd;  // both SAE buffers
+    c.cells.head[q + c.WH + 1] = hd;  // (buffer 1 follows buffer 0's guard head)
 }
 
 // lastEventTime surface for farms_get_last_event_time: stamp of the latest
@@ -3214,8 +3304,8 @@ struct farms_handle {
     int fit_chunk = kDefaultFitChunk, pool_chunk = kDefaultPoolChunk;
     hipStream_t stream = nullptr;
     // persistent surfaces (x-major, W*H cells)
-    SaeHead *sae_head = nullptr;  // two buffers of WH heads (fit-chunk parity), then
-    SaeTail *sae_tail = nullptr;  // two of WH tails
+    SaeHead *sae_head = nullptr;  // two buffers of WH + 1 heads (fit-chunk parity; the last one a zero guard), then
+    SaeTail *sae_tail = nullptr;  // two of WH + 1 tails
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
     // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1), indexed by
@@ -3467,8 +3557,10 @@ int reset_surfaces(farms_handle *h) {
     int rc = sync_all(h);
     if (rc) return rc;
     // tag 0: never visited, never touched (chunk seqs start at 1)
-    HIPCHK(hipMemsetAsync(h->sae_head, 0, 2 * sizeof(SaeHead) * h->WH, h->stream));  // both SAE buffers
-    HIPCHK(hipMemsetAsync(h->sae_tail, 0, 2 * sizeof(SaeTail) * h->WH, h->stream));
+    // both SAE buffers, each WH cells and a guard head (index WH, never written:
+    // the fit reads it for cells outside the stored region)
+    HIPCHK(hipMemsetAsync(h->sae_head, 0, 2 * sizeof(SaeHead) * (h->WH + 1), h->stream));
+    HIPCHK(hipMemsetAsync(h->sae_tail, 0, 2 * sizeof(SaeTail) * (h->WH + 1), h->stream));
     HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
     HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
     for (Work &w : h->ws) {
@@ -3837,7 +3929,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     const uint32_t seq_base = h->seq;
     h->seq += (uint32_t)n_fit_chunks;
     auto cells_of = [&](int f) {
-        const size_t o = (size_t)(f & 1) * (size_t)h->WH;
+        const size_t o = (size_t)(f & 1) * (size_t)(h->WH + 1);  // (WH cells and the guard head)
         return SaeBuf{h->sae_head + o, h->sae_tail + o};
     };
     auto fit_start = [&](int f) { return f * h->fit_chunk; };
@@ -4088,6 +4180,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     *out = nullptr;
     if (prm->width <= 0 || prm->height <= 0 || (int64_t)prm->width * prm->height > kMaxSlots)
         return fail(FARMS_EINVAL, "sensor size out of range (at most 2^24 - 256 pixels)");
+    if (prm->width > 65535 || prm->height > 65535)  // (the fit's AtA products are 24-bit: coordinates < 2^16)
+        return fail(FARMS_EINVAL, "sensor width and height must be below 65536");
     if (prm->window_jump <= 0 || prm->max_window < 0) return fail(FARMS_EINVAL, "bad pooling scales");
     if (prm->region_width < 0 || (prm->region_width > 0 && (prm->region_x0 < 0 || prm->region_x0 + prm->region_width > prm->width)))
         return fail(FARMS_EINVAL, "stored region outside the sensor");
@@ -4203,7 +4297,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
             if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess)
                 return bail(fail(FARMS_EHIP, "hipEventCreate"));
     }
-    if ((rc = dalloc(&h->sae_head, 2 * h->WH)) || (rc = dalloc(&h->sae_tail, 2 * h->WH)) ||
+    if ((rc = dalloc(&h->sae_head, 2 * (h->WH + 1))) || (rc = dalloc(&h->sae_tail, 2 * (h->WH + 1))) ||
         (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
@@ -4279,6 +4373,22 @@ extern "C" int farms_set_profiling(farms_handle *h, int enable) {
     h->counting = enable != 0 && enable != FARMS_PROF_TIMING && enable != FARMS_PROF_POOL;
     return FARMS_OK;
 }
+
+#ifdef FARMS_POOL_STAMPS
+// Diagnostic builds only: k_pool's per-phase cycle sums (g_pool_stamps), then cleared.
+extern "C" int farms_debug_pool_stamps(unsigned long long *out) {
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned long long> rows(8 * kStampRows, 0ull);
+    HIPCHK(hipMemcpyFromSymbol(rows.data(), HIP_SYMBOL(g_pool_stamps), sizeof(unsigned long long) * rows.size()));
+    for (int i = 0; i < 8; ++i) {
+        out[i] = 0;
+        for (int r = 0; r < kStampRows; ++r) out[i] += rows[8 * r + i];
+    }
+    std::fill(rows.begin(), rows.end(), 0ull);
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_pool_stamps), rows.data(), sizeof(unsigned long long) * rows.size()));
+    return FARMS_OK;
+}
+#endif
 
 extern "C" int farms_get_stats(const farms_handle *h, farms_stats *out) {
     if (!h || !out) return fail(FARMS_EINVAL, "null argument");

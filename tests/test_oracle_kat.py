@@ -197,3 +197,29 @@ def test_serial_mode_semantics():
     one = o.process(np.array([3], np.int32), np.array([4], np.int32), np.array([0], np.uint32),
                     np.array([1], np.int32))
     assert one["r_local"][0] == 0  # a lone event: DET < 1
+
+
+def test_eigen33_gemv_order_moves_bits_not_records():
+    """The oracle's Eigen switch (farms_oracle_set_eigen): 3.3's GEMV adds each
+    block of four columns of (A2*At)*Y as res + ((p0 + p3) + (p2 + p1)) on the
+    rows of a and b, 3.4 sums sequentially (vFlow.cpp:1338).  Filtersize 3 takes
+    Eigen's lazy product in both (n + 4 < 20): bitwise equal.  At filtersize 5
+    the last ulp of many local flows moves, while validity, scale and the 1e-4
+    bar hold (the full-size measurement: profiles/r05_eigen_sensitivity.log)."""
+    import farms
+    from parity import compare
+
+    for fs, cfg in ((3, 1), (5, 2)):
+        W, H = (128, 128) if cfg == 1 else (320, 320)
+        x, y, t, p = farms.synth_config(cfg, 40_000).relative()
+        a = OracleFlow(H, W, fs, 5, eigen=34).process(x, y, t, p)
+        b = OracleFlow(H, W, fs, 5, eigen=33).process(x, y, t, p)
+        same = np.array_equal(a["vx"].view(np.int64), b["vx"].view(np.int64))
+        if fs == 3:
+            assert same
+        else:
+            assert not same
+            rep = compare(b, a)
+            assert rep["ok"] and rep["valid_mismatch"] == 0 and rep["scale_mismatch"] == 0, rep
+    with pytest.raises(ValueError):
+        OracleFlow(320, 320, 5, 5, eigen=32)

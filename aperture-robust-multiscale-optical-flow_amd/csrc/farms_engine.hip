@@ -1392,23 +1392,54 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     // the union stamps were written by the other lanes of this wave's quad
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    auto cell = [&](int k, uint32_t &X, uint32_t &Y, uint32_t &T) {
-        const int kx = k / side, ky = k % side;
-        const bool vk = (vis >> k) & 1;  // never-visited cells store (0, 0): vFlow.cpp:1226-1233
-        X = vk ? (uint32_t)(bi + kx - FR) : 0u; Y = vk ? (uint32_t)(bj + ky - FR) : 0u;
-        T = ut[((ub + kx) * US + vb + ky) * kFitQS];
+    // This lane's window cells k = j, j + 4, ... (cx-major, k = kx * side + ky)
+    // through a cursor advanced by 4 cells: the stored coordinates (a
+    // never-visited cell stores (0, 0): vFlow.cpp:1226-1233) and the stamp in
+    // the union tile (slot ofs = (ub + kx) * US + vb + ky)
+    struct Cursor {
+        int kx, ky, ofs;
+        uint64_t vs;  // vis >> k
     };
-    // Y (vFlow.cpp:1229-1233); (t - 2^32) is exact in double, so selecting
-    // before the one multiply is the reference's expression
-    auto ytime = [&](uint32_t T) { return (T > te ? (double)T - kMaxStamp : (double)T) * kTsToSec; };
+    auto cursor = [&]() {
+        Cursor q;
+        q.kx = j / side;
+        q.ky = j % side;
+        q.ofs = (ub + q.kx) * US + vb + q.ky;
+        q.vs = vis >> j;
+        return q;
+    };
+    auto advance = [&](Cursor &q) {
+        q.ky += 4;
+        q.ofs += 4;
+        q.vs >>= 4;
+        if (q.ky >= side) { q.ky -= side; ++q.kx; q.ofs += US - side; }
+        if constexpr (side < 5)
+            if (q.ky >= side) { q.ky -= side; ++q.kx; q.ofs += US - side; }
+    };
+    auto cell = [&](const Cursor &q, uint32_t &X, uint32_t &Y, uint32_t &T) {
+        const uint32_t m = 0u - (uint32_t)(q.vs & 1);  // all ones if visited
+        X = (uint32_t)(bi + q.kx - FR) & m;
+        Y = (uint32_t)(bj + q.ky - FR) & m;
+        T = ut[q.ofs * kFitQS];
+    };
+    // Y (vFlow.cpp:1229-1233): t * 1e-6, or (t - 2^32) * 1e-6 for a stamp in the
+    // event's future; t - 2^32 and t + 0 are exact in double, so adding the
+    // selected offset before the one multiply is the reference's expression
+    auto ytime = [&](uint32_t T) { return ((double)T + (T > te ? -kMaxStamp : 0.0)) * kTsToSec; };
+    constexpr int NF = np / 4;  // full rounds of four cells (np % 4 == 1: one cell, lane 0's, after them)
     // AtA (vFlow.cpp:1307-1311): integer sums, exact in any split and order
     // (coordinates < 2^16: the 24-bit products are exact)
     int64_t sxx = 0, sxy = 0, sx = 0, syy = 0, sy = 0;
+    {
+        Cursor q = cursor();
 #pragma unroll 1
-    for (int k = j; k < np; k += 4) {
-        uint32_t X, Y, T;
-        cell(k, X, Y, T);
-        sxx += __umul24(X, X); sxy += __umul24(X, Y); sx += X; syy += __umul24(Y, Y); sy += Y;
+        for (int it = 0; it <= NF; ++it) {
+            uint32_t X, Y, T;
+            cell(q, X, Y, T);
+            if (it == NF && j != 0) X = Y = 0;  // past the window (adds nothing)
+            sxx += __umul24(X, X); sxy += __umul24(X, Y); sx += X; syy += __umul24(Y, Y); sy += Y;
+            advance(q);
+        }
     }
     sxx = quad_sum_i64(sxx); sxy = quad_sum_i64(sxy); sx = quad_sum_i64(sx);
     syy = quad_sum_i64(syy); sy = quad_sum_i64(sy);
@@ -1427,16 +1458,13 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
     const double cz = (double)te * kTsToSec;
     // (A2 * At) * Y in the reference order (r2, the intercept, is never used:
     // vFlow.cpp:1352-1377).  Each term m_k * yt_k is one rounded product,
-    // independent of the others, so lane j of the quad forms the terms of
-    // cells k = kb + j, and the sums then add them in order k = 0, 1, ... on
+    // independent of the others, so lane j of the quad forms the terms of its
+    // cells k = 4 it + j, and the sums then add them in order k = 0, 1, ... on
     // every lane (quad broadcasts): the additions are the reference's, a quarter
     // of the products per lane.
-    double r0 = 0.0, r1 = 0.0;
-#pragma unroll 1
-    for (int kb = 0; kb < np; kb += 4) {
-        const int k = kb + j < np ? kb + j : np - 1;
+    auto terms = [&](const Cursor &q, double &q0, double &q1) {
         uint32_t Xi, Yi, T;
-        cell(k, Xi, Yi, T);
+        cell(q, Xi, Yi, T);
         const double X = (double)Xi, Y = (double)Yi, yt = ytime(T);
         double m0, m1;
         if (gemm) {
@@ -1446,27 +1474,48 @@ __device__ __forceinline__ void fit_event_quad_u(const Ctx &c, int4 fd, uint32_t
             m0 = (d0 * X + d3 * Y) + d6 * 1.0;
             m1 = (d1 * X + d4 * Y) + d7 * 1.0;
         }
-        const double q0 = m0 * yt, q1 = m1 * yt;
-        const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
-        if (!gemv && kb == 0) { r0 = a0; r1 = a1; }
-        else { r0 = r0 + a0; r1 = r1 + a1; }
-        if (kb + 1 < np) { r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1); }
-        if (kb + 2 < np) { r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1); }
-        if (kb + 3 < np) { r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1); }
+        q0 = m0 * yt;
+        q1 = m1 * yt;
+    };
+    double r0 = 0.0, r1 = 0.0;
+    {
+        Cursor q = cursor();
+#pragma unroll 1
+        for (int it = 0; it < NF; ++it) {
+            double q0, q1;
+            terms(q, q0, q1);
+            const double a0 = quad_bcast<0>(q0), a1 = quad_bcast<0>(q1);
+            if (!gemv && it == 0) { r0 = a0; r1 = a1; }
+            else { r0 = r0 + a0; r1 = r1 + a1; }
+            r0 = r0 + quad_bcast<1>(q0); r1 = r1 + quad_bcast<1>(q1);
+            r0 = r0 + quad_bcast<2>(q0); r1 = r1 + quad_bcast<2>(q1);
+            r0 = r0 + quad_bcast<3>(q0); r1 = r1 + quad_bcast<3>(q1);
+            advance(q);
+        }
+        // the last cell, k = np - 1 = 4 NF: lane 0's (the other lanes' cursors
+        // are past the window and read some slot of the union tile: unused)
+        double q0, q1;
+        terms(q, q0, q1);
+        r0 = r0 + quad_bcast<0>(q0);
+        r1 = r1 + quad_bcast<0>(q1);
     }
     if (gemv) { r0 = r0 + 0.0; r1 = r1 + 0.0; }
     const double dtdp = sqrt(r0 * r0 + r1 * r1);  // vFlow.cpp:1349-1377 (pow(v,2.0) as v*v)
     const double half = dtdp / 2;
     const double ccx = (double)ex, ccy = (double)ey;
     int inliers = 0;
+    {
+        Cursor q = cursor();
 #pragma unroll 1
-    for (int k = j; k < np; k += 4) {
-        uint32_t Xi, Yi, T;
-        cell(k, Xi, Yi, T);
-        const double yt = ytime(T);
-        const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
-        const double actualdt = yt - cz;
-        if (fabs(planedt - actualdt) < half && yt > 0) ++inliers;
+        for (int it = 0; it <= NF; ++it) {
+            uint32_t Xi, Yi, T;
+            cell(q, Xi, Yi, T);
+            const double yt = ytime(T);
+            const double planedt = (r0 * ((double)Xi - ccx) + r1 * ((double)Yi - ccy));
+            const double actualdt = yt - cz;
+            if (fabs(planedt - actualdt) < half && yt > 0 && (it < NF || j == 0)) ++inliers;
+            advance(q);
+        }
     }
     inliers += xch32<0>(inliers);
     inliers += xch32<1>(inliers);

@@ -3171,6 +3171,456 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Paired pooling (round 5): two valid events per wavefront, 32 lanes each.
+// The fold is one exec-masked v_add_f64 per staged entry whatever the number
+// of scales, so one event per wave issued ~157 fold instructions per valid
+// event at C3 with 44 of 64 lanes in use; two events share each instruction
+// when an event needs at most 32 lanes: quantities {L, L cos, L sin} of scales
+// 1..K-1 on lanes 3 (k - 1) + q of the event's half (K <= 11: 30 lanes; lanes
+// 30, 31 fold padding), the contributor counts from an integer histogram of
+// the entries' smallest scales, and scale 0 -- the event's own cell, the one
+// cell at distance 0 (an aliased second visit of it has d >= 1) -- from that
+// entry's values (0 + v, vFlow.cpp:1005-1008: v itself).  Every per-scale sum
+// is still the reference's sequence of additions: scale k's lane adds the
+// entries with k0 <= k in raster order from 0 (pool_one's guarantees), so the
+// records are bitwise k_pool's (tested).  The pass runs 32 candidates of each
+// event per step; the events of a pair are consecutive pooled events of one
+// pooling chunk in work order (k_pool_compact), so their windows overlap and
+// their step counts match.
+constexpr int kPairSlots = 40;  // staged entries per event: <= 32 per step + < 8 carried
+template <int K>
+constexpr bool kPairPool = K >= 2 && K <= 11;
+constexpr uint32_t kPairJunk = 0x1E1E1E1Eu;  // four shift bytes of 30: the half's lanes 30, 31 only
+// LDS of a paired-pooling wave, per event: segment-start bitmap, row segments,
+// staged {L, L cos, L sin} and shift bytes, the smallest-scale histogram, the
+// own cell's entry
+__host__ __device__ constexpr int pair_half_words(int bw, int rs) {
+    return bw + rs + 3 * kPairSlots + kPairSlots / 8 + 8 /* hist: 16 ints */ + 4 /* own: L, Lc, Ls, flag */;
+}
+
+// Ordered compaction of each pooling chunk's pooled events (valid flow, owned
+// column) to the front of its work-order positions: qe[cs + r] = the r-th one's
+// {event, x, y, t}, nv[ch] = their number.  One 256-thread block per chunk.
+__global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, int32_t *nv) {
+    __shared__ int s_wsum[4];
+    const int ch = ch0 + (int)blockIdx.x;
+    if (ch >= ch1) return;
+    const int cs = ch * c.C2, ce = min(cs + c.C2, c.n);
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    int carry = 0;
+    for (int base = cs; base < ce; base += 256) {
+        const int w = base + tid;
+        bool ok = false;
+        int4 fd = make_int4(0, 0, 0, 0);
+        if (w < ce) {
+            fd = c.fdesc[w];
+            ok = c.valid[fd.x] && fd.y >= c.own_lo && fd.y < c.own_hi;
+        }
+        const uint64_t bal = __ballot(ok);
+        if (lane == 0) s_wsum[wv] = (int)__popcll(bal);
+        __syncthreads();
+        int off = carry;
+        for (int i = 0; i < wv; ++i) off += s_wsum[i];
+        const int tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+        if (ok) c.qe[cs + off + (int)__popcll(bal & lt)] = fd;
+        __syncthreads();  // (s_wsum is rewritten next round)
+        carry += tot;
+    }
+    if (tid == 0) nv[ch] = carry;
+}
+
+// Inclusive prefix sum within each 32-lane half (wave_incl_scan without its
+// last, half-crossing step).
+__device__ __forceinline__ int half_incl_scan(int v) {
+    const int lane = (int)__lane_id(), rl = lane & 15;
+    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    if (rl >= 1) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    if (rl >= 2) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    if (rl >= 4) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    if (rl >= 8) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15 (rows 1, 3 from rows 0, 2)
+    if ((lane & 31) >= 16) v += t;
+    return v;
+}
+
+// Max within each 32-lane half (exact).
+__device__ __forceinline__ double half_max(double v) {
+    v = fmax(v, xch<0>(v));
+    v = fmax(v, xch<1>(v));
+    v = fmax(v, xch<2>(v));
+    v = fmax(v, xch<3>(v));
+    v = fmax(v, xch<4>(v));
+    return v;
+}
+
+// pool_rows for two windows: half h builds its event's row table (rows hl,
+// hl + 32, hl + 64, hl + 96) into its own LDS arrays; returns the half's
+// flattened length (0 for an absent event).
+__device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool act, int i_lo, int nrows, int j_lo,
+                                          int j_hi, uint64_t *s_start, uint32_t *s_row) {
+    const int H = c.H;
+    const int WHl = (int)c.WH, OFF = c.X0 * c.H;
+    const int WHs = (int)c.WHs;
+    const int hl = lane & 31;
+    const uint64_t hm = lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
+    uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
+    {
+        const int nw = act ? ((nrows * (j_hi - j_lo + 1) + 63) >> 6) + 1 : 0;
+        for (int i = hl; i < nw; i += 32) s_start[i] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    constexpr int NB = 4;  // row batches: 2M + 1 <= 127 rows
+    const BmWord *bwb = c.bw_ring + (int64_t)buf * c.nwords;
+    const int wmax = (int)c.nwords - 1;
+    int lo_[NB], hi0_[NB], hi1_[NB], gb_[NB];
+    bool has_[NB], str_[NB];
+    uint64_t bA[NB], bB[NB], bC[NB];
+    uint32_t oA[NB], oB[NB], oC[NB];
+#pragma unroll
+    for (int hh = 0; hh < NB; ++hh) {
+        const int r = hl + 32 * hh;
+        const int base = (i_lo + (r < nrows ? r : 0)) * H;
+        int l1 = base + j_hi;
+        if (l1 > WHs - 1) l1 = WHs - 1;  // past the end of the sensor: no contribution
+        int l0 = base + j_lo - OFF;
+        l1 -= OFF;
+        if (l0 < 0) l0 = 0;               // outside the stored region: never visited
+        if (l1 > WHl - 1) l1 = WHl - 1;
+        const int gb = l1 & ~(kGroupCells - 1);
+        has_[hh] = act && r < nrows && l0 <= l1;
+        str_[hh] = has_[hh] && l0 < gb;
+        lo_[hh] = l0; gb_[hh] = gb;
+        hi0_[hh] = str_[hh] ? gb - 1 : l1;
+        hi1_[hh] = l1;
+        const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
+                  wc = min(max(l1 >> 6, 0), wmax);
+        const BmWord A = at32(bwb, (uint32_t)wa), B = at32(bwb, (uint32_t)wb), C = at32(bwb, (uint32_t)wc);
+        bA[hh] = A.bm; oA[hh] = A.wo;
+        bB[hh] = B.bm; oB[hh] = B.wo;
+        bC[hh] = C.bm; oC[hh] = C.wo;
+    }
+    int carry = 0, nz = 0;
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int hh = 0; hh < NB; ++hh) {
+        const int r = hl + 32 * hh;
+        const int lo = (int)(oA[hh] + (uint32_t)__popcll(bA[hh] & ((1ull << (lo_[hh] & 63)) - 1)));
+        const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
+        const int h1 = (int)(oC[hh] + (uint32_t)__popcll(bC[hh] & ((2ull << (hi1_[hh] & 63)) - 1)));
+        const int n0 = has_[hh] ? h0 - lo : 0;
+        const int n1 = str_[hh] ? h1 - gb_[hh] : 0;
+        const int cnt = n0 + n1;
+        const int incl = half_incl_scan(cnt);
+        const int start = carry + incl - cnt;
+        const uint64_t b0 = __ballot(n0 > 0) & hm, b1 = __ballot(n1 > 0) & hm;
+        int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
+        if (n0 > 0) {
+            s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
+            atomicOr(&sbits[start >> 5], 1u << (start & 31));
+        }
+        if (n1 > 0) {
+            const int st1 = start + n0;
+            s_row[idx] = ((uint32_t)r << 25) | (uint32_t)(gb_[hh] - st1 + kRowBias);
+            atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
+        }
+        nz += (int)__popcll(b0) + (int)__popcll(b1);
+        const int tA = __builtin_amdgcn_readlane(incl, 31), tB = __builtin_amdgcn_readlane(incl, 63);
+        carry += lane < 32 ? tA : tB;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return carry;
+}
+
+// Fold of 8 entry slots of both events: slot u adds event A's entry on the
+// lanes of A's half selected by byte u of a0:a1 (lanes >= 3 (k0 - 1) of the
+// half: the scales containing the entry; 30: padding, the half's junk lanes)
+// and B's likewise from b0:b1 (exec_lo, exec_hi), one v_add_f64 for both.  As
+// fold8_salu: a full exec at entry, SCC clobbered, exec restored.
+__device__ __forceinline__ void fold8_pair(double &acc, uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
+                                           const double (&v)[8]) {
+    uint64_t sv;
+    uint32_t ta, tb;
+#define FARMS_PAIR_SLOT(WA, WB, SH, V)                                                             \
+    "s_lshr_b32 %[ta], %[" WA "], " SH "\n"                                                        \
+    "s_lshr_b32 %[tb], %[" WB "], " SH "\n"                                                        \
+    "s_lshl_b32 exec_lo, -1, %[ta]\n"                                                              \
+    "s_lshl_b32 exec_hi, -1, %[tb]\n"                                                              \
+    "v_add_f64 %[acc], %[acc], %[" V "]\n"
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n"
+        FARMS_PAIR_SLOT("a0", "b0", "0", "v0") FARMS_PAIR_SLOT("a0", "b0", "8", "v1")
+        FARMS_PAIR_SLOT("a0", "b0", "16", "v2") FARMS_PAIR_SLOT("a0", "b0", "24", "v3")
+        FARMS_PAIR_SLOT("a1", "b1", "0", "v4") FARMS_PAIR_SLOT("a1", "b1", "8", "v5")
+        FARMS_PAIR_SLOT("a1", "b1", "16", "v6") FARMS_PAIR_SLOT("a1", "b1", "24", "v7")
+        "s_mov_b64 exec, %[sv]\n"
+        : [acc] "+v"(acc), [sv] "=&s"(sv), [ta] "=&s"(ta), [tb] "=&s"(tb)
+        : [a0] "s"(a0), [a1] "s"(a1), [b0] "s"(b0), [b1] "s"(b1), [v0] "v"(v[0]), [v1] "v"(v[1]),
+          [v2] "v"(v[2]), [v3] "v"(v[3]), [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7])
+        : "scc");
+#undef FARMS_PAIR_SLOT
+}
+
+// The candidate pass and the scale choice of a pair (pool_one / pool_finish
+// for two events): lanes of half h work on event h (its fields per lane).
+template <int K>
+__device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int e, int ex, int ey, uint32_t teu,
+                                          int buf, int row_i0, int total, int totA, int totB,
+                                          const uint64_t *s_start, const uint32_t *s_row, double *s_val,
+                                          uint8_t *s_k0, int *s_hist, double *s_own) {
+    static_assert(kPairPool<K>, "paired pooling: 3 (K - 1) <= 30 lanes per event");
+    const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
+    const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
+    const int H = c.H, J = c.J;
+    const int OFF = c.X0 * c.H;
+    const int hl = lane & 31;
+    const uint64_t hm = lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
+    const uint64_t lt = (1ull << lane) - 1;
+    // serial mode: the own cell is pooled with the stamp its lastEventTime
+    // still holds (vFlow.cpp:790 vs :264)
+    const uint32_t own_lin = c.serial ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
+    const uint32_t own_tprev = c.serial ? (uint32_t)c.link[e].w : 0u;
+    // this lane's fold: quantity q of scale kk (lanes 30, 31 of the half: junk)
+    const int q = hl % 3;
+    // the half's histogram and own entry start empty
+    if (hl < 16) s_hist[hl] = 0;
+    if (hl < 4) s_own[hl] = 0.0;
+    double acc = 0.0;
+    int ncon = 0;
+    const double *const vdummy = reinterpret_cast<const double *>(c.evf + e);
+    int mbase = 0;
+    // flattened position f0 + hl of this half's window
+    auto locate = [&](int f0, int &row, int &k) {
+        const uint64_t mk = s_start[f0 >> 6];
+        const int bit = (f0 & 63) + hl;
+        const int m = mbase + (int)__popcll(mk & ((2ull << bit) - 1)) - 1;
+        if ((f0 & 63) == 32) mbase += (int)__popcll(mk);
+        const uint32_t rs = s_row[m < 0 ? 0 : m];
+        row = (int)(rs >> 25);
+        k = f0 + hl + (int)(rs & 0x1FFFFFFu) - kRowBias;
+    };
+    const int tmax = totA > totB ? totA : totB;  // (wave-uniform)
+    // a valid candidate index for lanes past their window's end (lane 0's or
+    // lane 32's, whichever half is still scanning)
+    auto safe_k = [&](int f0, int k) {
+        const int kA = __builtin_amdgcn_readlane(k, 0), kB = __builtin_amdgcn_readlane(k, 32);
+        return (uint32_t)(f0 < totA ? kA : kB);
+    };
+    int rc = 0, kc = 0;
+    CandHdr hc{};
+    if (tmax > 0) {
+        locate(0, rc, kc);
+        const uint32_t sk = safe_k(0, kc);
+        hc = at32(chdr, act && hl < total ? (uint32_t)kc : sk);
+    }
+    uint64_t pbal = 0;
+    double pv0 = 0.0, pv1 = 0.0, pv2 = 0.0;
+    int pk0 = K;
+    int stA = 0, stB = 0;  // (wave-uniform) staged entries not yet folded, per event
+    for (int f0 = 0;; f0 += 32) {
+        const bool have = f0 < tmax;  // wave-uniform
+        bool con = false;
+        int k0 = K;
+        const double *vp = vdummy;
+        if (have && act && f0 + hl < total) {
+            const CandHdr &hd = hc;
+            uint32_t tq;
+            bool ok;
+            if (hd.e1 > e) { ok = (hd.lin & kCandSnapOk) != 0; tq = hd.t_snap; vp = &cval[kc].L_snap; }
+            else if (!(hd.lin & kCandMore)) { ok = (hd.lin & kCandOneOk) != 0; tq = hd.t1; vp = &cval[kc].L1; }
+            else if (!(hd.lin & kCandMore2)) {
+                const int2 r2 = *reinterpret_cast<const int2 *>(&cval[kc].run_lo);
+                const int e2 = r2.x & 0x7FFFFFFF;
+                if (e2 > e) { ok = (hd.lin & kCandOneOk) != 0; tq = hd.t1; vp = &cval[kc].L1; }
+                else { ok = r2.x < 0; tq = (uint32_t)r2.y; vp = &c.evf[e2].L; }
+            } else {
+                const CandVal &cv = cval[kc];
+                const int sev = c.P[run_search_bounds(c, cv.run_lo, cv.run_hi, e)];
+                const FlowCell fe = c.evf[sev];
+                ok = fe.L > 0; tq = fe.t; vp = &c.evf[sev].L;
+            }
+            if ((hd.lin & kCandLinMask) == own_lin) tq = own_tprev;
+            const int64_t dt = (int64_t)teu - (int64_t)tq;  // |t_e - t_cell| < 500 us (vFlow.cpp:1002/1115)
+            const int i = row_i0 + rc;
+            const int j = (int)(hd.lin & kCandLinMask) + OFF - (int)__umul24((uint32_t)i, (uint32_t)H);
+            if (ok && (uint64_t)(dt + 499) < 999u) {
+                const int di = i > ex ? i - ex : ex - i, dj = j > ey ? j - ey : ey - j;
+                const int d = di > dj ? di : dj;
+                k0 = J == 1 ? d : (int)__umulhi((uint32_t)(d + J - 1), c.kmagic);
+                con = true;
+            }
+        }
+        if (!con) vp = vdummy;
+        const double v0 = vp[0], v1 = vp[1], v2 = vp[2];
+        int rn = 0, kn = 0;
+        CandHdr hn = hc;
+        if (f0 + 32 < tmax) {  // (wave-uniform)
+            locate(f0 + 32, rn, kn);
+            const uint32_t sk = safe_k(f0 + 32, kn);
+            hn = at32(chdr, act && f0 + 32 + hl < total ? (uint32_t)kn : sk);
+        }
+        // ---- stage and fold the previous step's contributors of both events
+        if (pbal) {
+            const int cA = (int)__popcll(pbal & 0xFFFFFFFFull), cB = (int)__popcll(pbal >> 32);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if ((pbal >> lane) & 1) {
+                const int slot = (lane < 32 ? stA : stB) + (int)__popcll(pbal & lt & hm);
+                s_val[3 * slot] = pv0; s_val[3 * slot + 1] = pv1; s_val[3 * slot + 2] = pv2;
+                s_k0[slot] = (uint8_t)(pk0 > 0 ? 3 * (pk0 - 1) : 0);
+                atomicAdd(&s_hist[pk0], 1);
+                if (pk0 == 0) { s_own[0] = pv0; s_own[1] = pv1; s_own[2] = pv2; s_own[3] = 1.0; }
+            }
+            stA += cA;
+            stB += cB;
+            ncon += lane < 32 ? cA : cB;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const int wA = stA & ~7, wB = stB & ~7;
+            const int wmaxg = wA > wB ? wA : wB;
+            const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+#pragma unroll 1
+            for (int r = 0; r < wmaxg; r += 8) {
+                const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
+                double vv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (r + u) + q];
+                const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
+                const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
+                fold8_pair(acc, r < wA ? a0 : kPairJunk, r < wA ? a1 : kPairJunk, r < wB ? b0 : kPairJunk,
+                           r < wB ? b1 : kPairJunk, vv);
+            }
+            // carry each event's rest (< 8) to its slots [0, rest)
+            const int rA = stA - wA, rB = stB - wB;
+            const int w_h = lane < 32 ? wA : wB, r_h = lane < 32 ? rA : rB;
+            if ((wA > 0 && rA > 0) || (wB > 0 && rB > 0)) {
+                double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+                uint8_t mk = 0;
+                const bool mv = w_h > 0 && hl < r_h;
+                if (mv) {
+                    m0 = s_val[3 * (w_h + hl)]; m1 = s_val[3 * (w_h + hl) + 1]; m2 = s_val[3 * (w_h + hl) + 2];
+                    mk = s_k0[w_h + hl];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                if (mv) {
+                    s_val[3 * hl] = m0; s_val[3 * hl + 1] = m1; s_val[3 * hl + 2] = m2;
+                    s_k0[hl] = mk;
+                }
+            }
+            stA = rA;
+            stB = rB;
+        }
+        if (!have) break;
+        pbal = __ballot(con);
+        pv0 = v0; pv1 = v1; pv2 = v2;
+        pk0 = k0;
+        hc = hn; rc = rn; kc = kn;
+    }
+    if (stA > 0 || stB > 0) {  // the last groups, padded with junk entries
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int st_h = lane < 32 ? stA : stB;
+        if (hl >= st_h && hl < 8) s_k0[hl] = (uint8_t)30;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+        const uint32_t kw0 = k4p[0], kw1 = k4p[1];
+        double vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * u + q];
+        const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
+        const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
+        fold8_pair(acc, stA > 0 ? a0 : kPairJunk, stA > 0 ? a1 : kPairJunk, stB > 0 ? b0 : kPairJunk,
+                   stB > 0 ? b1 : kPairJunk, vv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // ---- the scale choice per half (vFlow.cpp:1023-1059): lane hl < K holds
+    // scale hl's mean; scale 0 is the own entry alone (0 + v = v), scale k >= 1
+    // lane 3 (k - 1) + q's sums; counts from the histogram (exact integers)
+    const int base = lane & 32;
+    const int kl = hl < K ? hl : 0;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt += k <= kl ? s_hist[k] : 0;
+    const bool own_ok = s_own[3] != 0.0;
+    const double len_k = __shfl(acc, base + 3 * (kl > 0 ? kl - 1 : 0), 64);
+    const double L_k = kl == 0 ? (own_ok ? s_own[0] : 0.0) : len_k;
+    const bool is_len = act && hl < K;
+    const double mean = is_len && cnt > 0 ? L_k / (double)cnt : 0.0;
+    const double maxv = half_max(mean);
+    const uint64_t win = __ballot(is_len && mean == maxv) & hm;
+    const int mi = maxv > 0 ? (int)__builtin_ctzll(win) - base : 0;
+    int cnt_mi = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt_mi += k <= mi ? s_hist[k] : 0;
+    const int src = base + 3 * (mi > 0 ? mi - 1 : 0);
+    const double sx_s = __shfl(acc, src + 1, 64), sy_s = __shfl(acc, src + 2, 64);
+    const double sx = mi == 0 ? s_own[1] : sx_s, sy = mi == 0 ? s_own[2] : sy_s;
+    if (act && hl == 0) {
+        double gx, gy;
+        int sc;
+        if (maxv > 0) {
+            gx = sx / (double)cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
+            gy = sy / (double)cnt_mi;
+            sc = mi * J;
+        } else {  // vFlow.cpp:1085-1094
+            const FlowCell self = c.evf[e];
+            gx = self.Lc; gy = self.Ls; sc = 0;
+        }
+        c.r_true[e] = gx;  // (RTrue, ThetaTrue) by k_true_polar
+        c.th_true[e] = gy;
+        c.scale[e] = sc;
+        if (c.dbg_tc) c.dbg_tc[e] = make_int2(total, ncon);
+    }
+}
+
+// Two pooled events of a pooling chunk per wavefront (kPairPool): pair p of
+// chunk ch takes its compacted events 2p and 2p + 1 (k_pool_compact); pairs
+// past the chunk's count leave at once.  Same occupancy cap as k_pool.
+template <int K, bool W7>
+__global__ __launch_bounds__(64) void k_pool2(Ctx c, int ch0, int ch1, const int32_t *nv) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
+    if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
+    else asm volatile("" ::: FARMS_POOL_FLOOR_6);
+    const int lane = threadIdx.x & 63;
+    const int ppc = c.C2 >> 1;  // pair slots per chunk
+    const int lb = work_block();
+    const int ch = ch0 + lb / ppc, p = lb % ppc;
+    if (ch >= ch1) return;
+    const int cnt = nv[ch];
+    if (2 * p >= cnt) return;
+    const bool hasB = 2 * p + 1 < cnt;
+    const int cs = ch * c.C2;
+    const bool act = lane < 32 || hasB;
+    const int4 d = c.qe[cs + 2 * p + (lane >= 32 && hasB ? 1 : 0)];
+    const int e = d.x, ex = d.y, ey = d.z;
+    const uint32_t teu = (uint32_t)d.w;
+    const int buf = (c.ring0 + ch) % c.NB;  // the pair's chunk's candidate buffer
+    // this half's LDS
+    const int hw = pair_half_words(c.pool_bw, c.pool_rs);
+    uint64_t *s_start = s_dyn + (lane >= 32 ? hw : 0);
+    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + c.pool_bw);
+    double *s_val = reinterpret_cast<double *>(s_start + c.pool_bw + c.pool_rs);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * kPairSlots);
+    int *s_hist = reinterpret_cast<int *>(s_k0 + kPairSlots);
+    double *s_own = reinterpret_cast<double *>(s_hist + 16);
+    const int W = c.W, M = c.M;
+    const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
+    const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
+    const int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    const int totA = __builtin_amdgcn_readlane(total, 0), totB = __builtin_amdgcn_readlane(total, 32);
+    pool_pair<K>(c, lane, act, e, ex, ey, teu, buf, i_lo, total, totA, totB, s_start, s_row, s_val, s_k0, s_hist,
+                 s_own);
+}
+
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
 // owned) event: k_pool leaves (Gx, Gy) in the r_true / theta_true columns.
 __global__ void k_true_polar(Ctx c, int e0, int e1) {
@@ -3332,6 +3782,7 @@ struct Work {
     uint32_t *cpmax = nullptr;                 // k_cand plan: prefix maximum of ctmax
     int32_t *cbk = nullptr;                    // k_cand plan: first chunk reaching each chunk's kill window
     int32_t *bstart = nullptr;                 // k_cand: per chunk, the work-order start of each column band
+    int32_t *nv = nullptr;                     // paired pooling: per chunk, its pooled events (k_pool_compact)
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
     int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
@@ -3453,7 +3904,7 @@ void free_workspace(Work &w) {
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
-    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart);
+    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart); dfree(w.nv);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -3486,7 +3937,7 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
         (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch)) || (rc = dalloc(&w.cpmax, nch)) ||
-        (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1)))) {
+        (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1))) || (rc = dalloc(&w.nv, nch))) {
         free_workspace(w);
         return rc;
     }
@@ -3658,6 +4109,35 @@ bool pool_w7(int fr) {
 }
 pool_launcher pool_for(int K, int fr) {
     return pool_w7(fr) ? pool_for_cap<true>(K) : pool_for_cap<false>(K);
+}
+// Paired pooling (k_pool2, 2 <= K <= 11): grid = pair slots of chunks [ch0, ch1).
+template <int K, bool W7>
+void launch_pool2(const Ctx &c, int ch0, int ch1, const int32_t *nv, hipStream_t s) {
+    const size_t lds = sizeof(uint64_t) * 2 * (size_t)pair_half_words(c.pool_bw, c.pool_rs);
+    hipLaunchKernelGGL((k_pool2<K, W7>), dim3((ch1 - ch0) * (c.C2 >> 1)), dim3(64), lds, s, c, ch0, ch1, nv);
+}
+typedef void (*pair_launcher)(const Ctx &, int, int, const int32_t *, hipStream_t);
+template <bool W7>
+pair_launcher pair_for_cap(int K) {
+    switch (K) {
+    case 2: return launch_pool2<2, W7>;   case 3: return launch_pool2<3, W7>;   case 4: return launch_pool2<4, W7>;
+    case 5: return launch_pool2<5, W7>;   case 6: return launch_pool2<6, W7>;   case 7: return launch_pool2<7, W7>;
+    case 8: return launch_pool2<8, W7>;   case 9: return launch_pool2<9, W7>;   case 10: return launch_pool2<10, W7>;
+    case 11: return launch_pool2<11, W7>;
+    default: return nullptr;  // one event per wave (k_pool)
+    }
+}
+// Pairs are the default beside the fs <= 5 fits: C3 75.4 -> 73.0 ms per step.
+// Beside the fs-7 fit (10.8 KB of LDS per wave, the sweep that paces C4/C5)
+// the pairs' 6.4 KB per wave cost fit waves: C4 54.5 -> 55.8 ms, so fs 7 keeps
+// one event per wave (profiles/r05_ab_pool_pairs.log).  FARMS_POOL_PAIRS=0|1
+// overrides (A/B and test aid; the same bits).  Pairs need even pooling chunks
+// (the pair slots of a chunk).
+pair_launcher pair_for(int K, int fr, int pool_chunk) {
+    bool on = fr <= 2;
+    if (const char *v = getenv("FARMS_POOL_PAIRS")) on = v[0] != '0';
+    if (!on || (pool_chunk & 1)) return nullptr;
+    return pool_w7(fr) ? pair_for_cap<true>(K) : pair_for_cap<false>(K);
 }
 // Tuning knobs of the fit (A/B aids; every choice gives the same bits):
 // FARMS_FIT_QUAD=0: one thread per event; FARMS_FIT_MODE 0 = re-gather the
@@ -3967,6 +4447,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         return FARMS_OK;
     };
     pool_launcher pl = pool_for(h->K, h->fr);
+    pair_launcher pl2 = pair_for(h->K, h->fr, h->pool_chunk);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const bool fit_quad = fit_quad_env();
     const int fit_mode = fit_mode_env();
@@ -4125,7 +4606,9 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             else
                 hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
         }
-        {
+        if (pl2) {  // pooled events compacted per chunk, for the pairs
+            hipLaunchKernelGGL(k_pool_compact, dim3(ch1 - ch0), dim3(256), 0, sc, c, ch0, ch1, w.nv);
+        } else {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
         }
@@ -4134,7 +4617,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (prof) { int rc = mark(h, sp, &k0); if (rc) return rc; }
-        pl(c, p0, p1, sp);
+        if (pl2) pl2(c, ch0, ch1, w.nv, sp);
+        else pl(c, p0, p1, sp);
         if (prof) {
             int rc = mark(h, sp, &k1);
             if (rc) return rc;
@@ -4460,10 +4944,11 @@ extern "C" int farms_kernel_info(const farms_handle *h, char *buf, int32_t len) 
     if (!fast) fit = "k_fit_wave";
     else if (!quad) fit = "k_fit<" + fr + ">";
     else fit = "k_fit_quad<" + fr + ">";
-    // the candidate build the last pooling call took (decided on the device per call)
+    // the candidate build the last pooling call enqueued (decided on the host, per call)
     const std::string cand = h->cand_last < 0 ? "" : h->cand_last ? "k_cand" : "k_chain";
+    const std::string pool = pair_for(h->K, h->fr, h->pool_chunk) ? "k_pool2" : "k_pool";
     const std::string js = "{\"fit\": \"" + fit + "\", \"fit_mode\": " + std::to_string(fast && quad ? mode : -1) +
-                           ", \"pool\": \"k_pool<" + std::to_string(h->K) + ">\", \"pool_cap\": " +
+                           ", \"pool\": \"" + pool + "<" + std::to_string(h->K) + ">\", \"pool_cap\": " +
                            (pool_w7(h->fr) ? "7" : "6") + ", \"cand_last\": \"" + cand + "\"}";
     std::snprintf(buf, (size_t)len, "%s", js.c_str());
     return FARMS_OK;

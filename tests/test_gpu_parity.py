@@ -643,3 +643,24 @@ def test_fit_streams_on_device_paths_are_bitwise_identical(fs, monkeypatch):
             with farms.FlowManager(720, 1280, fs, 5, fit_chunk=8192) as fm:
                 g = _device_run(fm, x, y, t, p, splits, two_phase)
             assert bitwise_equal(ref, g), (streams, two_phase, compare(ref, g))
+
+
+@pytest.mark.parametrize("jump,maxw,pc", [(50, 50, 0), (25, 50, 0), (10, 50, 2048), (5, 50, 0), (4, 50, 0), (5, 20, 1024)])
+def test_paired_pooling_is_bitwise_one_event_per_wave(jump, maxw, pc, monkeypatch):
+    """k_pool2 pools two events per wave (K <= 11 scales: 3 (K - 1) lanes per
+    event, counts from a histogram, scale 0 from the own entry) and k_pool one
+    (FARMS_POOL_PAIRS=0, and every K > 11 or odd pooling chunk): the same bits,
+    for 2 to 13 scales, an odd-sized last pair and partial last chunks."""
+    ev = farms.synth_config(3, 150_001)
+    x, y, t, p = ev.relative()
+    K = maxw // jump + 1
+    outs = {}
+    for pairs in ("1", "0"):
+        monkeypatch.setenv("FARMS_POOL_PAIRS", pairs)
+        with farms.FlowManager(720, 1280, 5, 5, window_jump=jump, max_window=maxw, pool_chunk=pc) as fm:
+            outs[pairs] = fm.process(x, y, t, p)
+            kern = fm.kernel_info()["pool"]
+        want = "k_pool2<" if pairs == "1" and 2 <= K <= 11 else "k_pool<"
+        assert kern.startswith(want), (kern, K)
+    assert bitwise_equal(outs["1"], outs["0"]), compare(outs["0"], outs["1"])
+    assert int((outs["1"].r_true != 0).sum()) > 1000

@@ -2524,7 +2524,13 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
         const int wi = (int)((q - qa) >> 6);
         const uint32_t slot = word_off(wi) + (uint32_t)__popcll(s_bm[wi] & ((1ull << (q & 63)) - 1));
         hr[slot] = hd;
-        vr[slot] = v;
+        if (item >= cs) {
+            vr[slot] = v;
+        } else {  // untouched in the chunk (e1 = INT_MAX): the pooling reads the snapshot only
+            vr[slot].L_snap = v.L_snap;
+            vr[slot].Lc_snap = v.Lc_snap;
+            vr[slot].Ls_snap = v.Ls_snap;
+        }
     }
 }
 
@@ -3595,12 +3601,16 @@ __global__ __launch_bounds__(64) void k_pool2(Ctx c, int ch0, int ch1, const int
     const int lb = work_block();
     const int ch = ch0 + lb / ppc, p = lb % ppc;
     if (ch >= ch1) return;
+    const int cs = ch * c.C2;
+    // the descriptor load goes out with the count's (clamped: a partial last
+    // chunk's pair slots reach past the call's events)
+    const int4 dq = c.qe[min(cs + 2 * p + (lane >> 5), c.n - 1)];
     const int cnt = nv[ch];
     if (2 * p >= cnt) return;
     const bool hasB = 2 * p + 1 < cnt;
-    const int cs = ch * c.C2;
     const bool act = lane < 32 || hasB;
-    const int4 d = c.qe[cs + 2 * p + (lane >= 32 && hasB ? 1 : 0)];
+    const int4 d = act ? dq : make_int4(__builtin_amdgcn_readfirstlane(dq.x), __builtin_amdgcn_readfirstlane(dq.y),
+                                        __builtin_amdgcn_readfirstlane(dq.z), __builtin_amdgcn_readfirstlane(dq.w));
     const int e = d.x, ex = d.y, ey = d.z;
     const uint32_t teu = (uint32_t)d.w;
     const int buf = (c.ring0 + ch) % c.NB;  // the pair's chunk's candidate buffer
@@ -5268,8 +5278,13 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     double *const ucol[6] = {out->r_true, out->theta_true, out->vx, out->vy, out->r_local, out->theta_local};
     int32_t *const uecho[4] = {out->x, out->y, out->t, out->p};
     for (int k = 0; k < 6; ++k) all_pinned &= (pin_col[k] = is_pinned(ucol[k]));
-    const char *edv = getenv("FARMS_ECHO_DMA");  // A/B aid: 0 = the x/y/t/p echo by host copies
-    const bool echo_dma = !(edv && edv[0] == '0');
+    // the x/y/t/p echo (vFlow.cpp:370-373) by host copies from the caller's
+    // inputs, not by D2H from the device copies: 16 B/event less PCIe traffic
+    // under the kernels (round 5, C3: the pinned leg, whose echo was DMAed,
+    // ran 89.0 ms against 82.2 for the pageable one, whose echo was copied on
+    // the host).  FARMS_ECHO_DMA=1: by D2H (A/B aid).
+    const char *edv = getenv("FARMS_ECHO_DMA");
+    const bool echo_dma = edv && edv[0] == '1';
     for (int k = 0; k < 4; ++k) all_pinned &= (pin_echo[k] = echo_dma && is_pinned(uecho[k]));
     const bool pin_scale = is_pinned(out->scale);
     all_pinned &= pin_scale;

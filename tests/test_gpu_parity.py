@@ -354,8 +354,9 @@ def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
 def test_host_path_pipeline_knobs_are_bitwise_invariant(subs, echo, monkeypatch):
     """The host path's pipeline knobs change only how the work is cut and
     moved: FARMS_SUBBATCHES (one call, or n/k events per sub-batch) and
-    FARMS_ECHO_DMA=0 (the x/y/t/p echo into pinned record columns by host
-    copies instead of D2H) give bitwise the default's records."""
+    FARMS_ECHO_DMA (1: the x/y/t/p echo into pinned record columns by D2H from
+    the device copies; 0, the default since round 5: by host copies from the
+    inputs) give bitwise the default's records."""
     ev = farms.synth_config(3, 2_000_000)
     x, y, t, p = ev.relative()
     keep = []

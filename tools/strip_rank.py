@@ -98,7 +98,8 @@ for r in ranks:
             hb = halo[(halo >= lo) & (halo < hi)]
             subs.append((lo, hi, torch.from_numpy((hb - lo).astype(np.int32)).to(dev),
                          hflows[torch.from_numpy(hb).to(dev)].contiguous()))
-    if a.split == "segments":  # the surfaces of the ranks before this one: stand-ins of the right shape
+    seg = a.split == "segments" and sh.seg is not None  # (N = 1: the whole stream, one call)
+    if seg:  # the surfaces of the ranks before this one: stand-ins of the right shape
         mine = torch.empty((2, W * H), dtype=torch.int64, device=dev)
         rows = max(len(segments.merge_rows(r)), 1)
         stack = torch.full((rows, W * H), -1, dtype=torch.int64, device=dev)
@@ -127,7 +128,7 @@ for r in ranks:
                 if b + 1 < len(subs):
                     exchange(b + 1)
             return
-        if a.split == "segments":
+        if seg:
             fm.last_stamps(dx[o:], dy[o:], dt[o:], sh.n_head, mine[0], mine[1])
             if r > 0:
                 fm.merge_stamps(stack, sae)

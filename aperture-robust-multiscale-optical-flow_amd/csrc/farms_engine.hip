@@ -3204,6 +3204,15 @@ constexpr uint32_t kPairJunk = 0x1E1E1E1Eu;  // four shift bytes of 30: the half
 __host__ __device__ constexpr int pair_half_words(int bw, int rs) {
     return bw + rs + 3 * kPairSlots + kPairSlots / 8 + 8 /* hist: 16 ints */ + 4 /* own: L, Lc, Ls, flag */;
 }
+// Timing experiment only (FARMS_PAIR_BITCAP=T builds, never the product): the
+// segment-start bitmap sized for T flattened positions; a wider window's event
+// is skipped (wrong records), to measure what the LDS saved buys.
+#ifndef FARMS_PAIR_BITCAP
+#define FARMS_PAIR_BITCAP 0
+#endif
+__host__ __device__ constexpr int pair_bw(int bw) {
+    return FARMS_PAIR_BITCAP > 0 && bw > FARMS_PAIR_BITCAP / 64 + 1 ? FARMS_PAIR_BITCAP / 64 + 1 : bw;
+}
 
 // Ordered compaction of each pooling chunk's pooled events (valid flow, owned
 // column) to the front of its work-order positions: qe[cs + r] = the r-th one's
@@ -3276,7 +3285,8 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
     const uint64_t hm = lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
     uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
     {
-        const int nw = act ? ((nrows * (j_hi - j_lo + 1) + 63) >> 6) + 1 : 0;
+        int nw = act ? ((nrows * (j_hi - j_lo + 1) + 63) >> 6) + 1 : 0;
+        if (FARMS_PAIR_BITCAP > 0 && nw > FARMS_PAIR_BITCAP / 64 + 1) nw = FARMS_PAIR_BITCAP / 64 + 1;
         for (int i = hl; i < nw; i += 32) s_start[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -3328,12 +3338,12 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
         if (n0 > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
-            atomicOr(&sbits[start >> 5], 1u << (start & 31));
+            if (FARMS_PAIR_BITCAP == 0 || start < FARMS_PAIR_BITCAP) atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
         if (n1 > 0) {
             const int st1 = start + n0;
             s_row[idx] = ((uint32_t)r << 25) | (uint32_t)(gb_[hh] - st1 + kRowBias);
-            atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
+            if (FARMS_PAIR_BITCAP == 0 || st1 < FARMS_PAIR_BITCAP) atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
         }
         nz += (int)__popcll(b0) + (int)__popcll(b1);
         const int tA = __builtin_amdgcn_readlane(incl, 31), tB = __builtin_amdgcn_readlane(incl, 63);
@@ -3615,17 +3625,19 @@ __global__ __launch_bounds__(64) void k_pool2(Ctx c, int ch0, int ch1, const int
     const uint32_t teu = (uint32_t)d.w;
     const int buf = (c.ring0 + ch) % c.NB;  // the pair's chunk's candidate buffer
     // this half's LDS
-    const int hw = pair_half_words(c.pool_bw, c.pool_rs);
+    const int hw = pair_half_words(pair_bw(c.pool_bw), c.pool_rs);
     uint64_t *s_start = s_dyn + (lane >= 32 ? hw : 0);
-    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + c.pool_bw);
-    double *s_val = reinterpret_cast<double *>(s_start + c.pool_bw + c.pool_rs);
+    const int bwp = pair_bw(c.pool_bw);
+    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + bwp);
+    double *s_val = reinterpret_cast<double *>(s_start + bwp + c.pool_rs);
     uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 3 * kPairSlots);
     int *s_hist = reinterpret_cast<int *>(s_k0 + kPairSlots);
     double *s_own = reinterpret_cast<double *>(s_hist + 16);
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    const int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    if (FARMS_PAIR_BITCAP > 0 && total > FARMS_PAIR_BITCAP - 64) total = 0;  // (experiment: skipped)
     const int totA = __builtin_amdgcn_readlane(total, 0), totB = __builtin_amdgcn_readlane(total, 32);
     pool_pair<K>(c, lane, act, e, ex, ey, teu, buf, i_lo, total, totA, totB, s_start, s_row, s_val, s_k0, s_hist,
                  s_own);
@@ -3725,7 +3737,8 @@ __global__ void k_last_time(const SaeHead *cells, int64_t WH, double *out) {
 // Algorithmic-work counters for the roofline: U_loc per event,
 // U_pool per valid event, valid count.  Grid-stride, one atomic per block.
 __global__ void k_stats(Ctx c) {
-    unsigned long long nv = 0, usae = 0, upool = 0, ncand = 0, ncon = 0, nown = 0;
+    unsigned long long nv = 0, usae = 0, upool = 0, ncand = 0, ncon = 0, nown = 0, nwide = 0;
+    unsigned int smax = 0;
     const int fr = c.fr;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < c.n;
          e += (int64_t)gridDim.x * blockDim.x) {
@@ -3737,7 +3750,12 @@ __global__ void k_stats(Ctx c) {
         nown += own;
         if (c.valid[e] && own) {
             ++nv;
-            if (c.dbg_tc) { const int2 tc = c.dbg_tc[e]; ncand += (unsigned)tc.x; ncon += (unsigned)tc.y; }
+            if (c.dbg_tc) {
+                const int2 tc = c.dbg_tc[e];
+                ncand += (unsigned)tc.x; ncon += (unsigned)tc.y;
+                nwide += tc.x > 1024;
+                smax = max(smax, (unsigned)tc.x);
+            }
             const int i_lo = max(0, x - c.M), i_hi = min(c.W - 1, x + c.M);
             const int j_lo = max(0, y - c.M), j_hi = min(c.W - 1, y + c.M);
             for (int i = i_lo; i <= i_hi; ++i) {
@@ -3748,18 +3766,23 @@ __global__ void k_stats(Ctx c) {
             }
         }
     }
-    constexpr int NC = 6;
+    constexpr int NC = 8;  // sums, then the max (slot 7)
     __shared__ unsigned long long s[NC][256];
     s[0][threadIdx.x] = nv; s[1][threadIdx.x] = usae; s[2][threadIdx.x] = upool;
     s[3][threadIdx.x] = ncand; s[4][threadIdx.x] = ncon; s[5][threadIdx.x] = nown;
+    s[6][threadIdx.x] = nwide; s[7][threadIdx.x] = smax;
     __syncthreads();
     for (int st = blockDim.x / 2; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st)
-            for (int r = 0; r < NC; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
+        if ((int)threadIdx.x < st) {
+            for (int r = 0; r < NC - 1; ++r) s[r][threadIdx.x] += s[r][threadIdx.x + st];
+            s[7][threadIdx.x] = max(s[7][threadIdx.x], s[7][threadIdx.x + st]);
+        }
         __syncthreads();
     }
-    if (threadIdx.x == 0)
-        for (int r = 0; r < NC; ++r) atomicAdd(&c.counters[r], s[r][0]);
+    if (threadIdx.x == 0) {
+        for (int r = 0; r < NC - 1; ++r) atomicAdd(&c.counters[r], s[r][0]);
+        atomicMax(&c.counters[7], s[7][0]);
+    }
 }
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
@@ -3802,6 +3825,7 @@ struct Work {
     std::vector<hipEvent_t> sync_ev;           // dependency events of a call (no timing)
     hipEvent_t done = nullptr;                 // recorded after every use of the set by an asynchronous call
     hipEvent_t ready = nullptr;                // two-phase calls: the fits and the imported flows are in place
+    bool ready_host = false;                   // ... and the host has seen `ready` complete (export / import synced F)
     hipEvent_t fend = nullptr;                 // asynchronous calls: stream F's last work of the call
     bool busy = false;                         // `done` recorded and the set not yet reused
 };
@@ -4034,7 +4058,7 @@ int harvest(farms_handle *h) {
     if (h->counters_dirty) {
         for (hipStream_t s : {h->stream, h->s_chain, h->s_pool, h->s_copy})
             if (s) HIPCHK(hipStreamSynchronize(s));
-        unsigned long long cnt[6];
+        unsigned long long cnt[8];
         HIPCHK(hipMemcpy(cnt, h->counters, sizeof(cnt), hipMemcpyDeviceToHost));
         HIPCHK(hipMemset(h->counters, 0, sizeof(cnt)));
         h->acc.n_valid += (int64_t)cnt[0];
@@ -4043,6 +4067,8 @@ int harvest(farms_handle *h) {
         h->acc.pool_candidates += (double)cnt[3];
         h->acc.pool_contributors += (double)cnt[4];
         h->acc.n_owned += (int64_t)cnt[5];
+        h->acc.pool_scan_over_1k += (int64_t)cnt[6];
+        h->acc.pool_scan_max = std::max(h->acc.pool_scan_max, (int64_t)cnt[7]);
         h->counters_dirty = false;
     }
     return FARMS_OK;
@@ -4123,7 +4149,7 @@ pool_launcher pool_for(int K, int fr) {
 // Paired pooling (k_pool2, 2 <= K <= 11): grid = pair slots of chunks [ch0, ch1).
 template <int K, bool W7>
 void launch_pool2(const Ctx &c, int ch0, int ch1, const int32_t *nv, hipStream_t s) {
-    const size_t lds = sizeof(uint64_t) * 2 * (size_t)pair_half_words(c.pool_bw, c.pool_rs);
+    const size_t lds = sizeof(uint64_t) * 2 * (size_t)pair_half_words(pair_bw(c.pool_bw), c.pool_rs);
     hipLaunchKernelGGL((k_pool2<K, W7>), dim3((ch1 - ch0) * (c.C2 >> 1)), dim3(64), lds, s, c, ch0, ch1, nv);
 }
 typedef void (*pair_launcher)(const Ctx &, int, int, const int32_t *, hipStream_t);
@@ -4425,7 +4451,16 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     auto ev_pool = [&](int S) { return w.sync_ev[2 + n_fit_chunks + 3 * (size_t)S]; };
     auto super_end = [&](int S) { return (int)std::min<int64_t>((int64_t)(S + 1) * B * h->pool_chunk, n); };
     auto ev_pk = [&](int S) { return w.sync_ev[3 + n_fit_chunks + 3 * (size_t)S]; };  // k_pool(S) done
-    if (phase == 2) ev_prep = w.ready;  // prepared by phase 1: its fits and the imported flows are in place
+    // phase 2: prepared by phase 1, its fits and the imported flows in place.
+    // When an export / import has already drained stream F past `ready`, the
+    // chain stream waits for nothing: a wait on that (completed) event, with
+    // the next sub-batch's fits enqueued on F behind it since, held the chain
+    // and the pooling until those fits had finished -- the fits and the
+    // pooling of the x-strip pipeline then ran in turns instead of together
+    // (C4 N=4 middle strip 79.7 ms, rocprofv3 timeline in
+    // profiles/r05_strip_trace_c4.txt; host call times in
+    // profiles/r05_strip_host_times.log).
+    if (phase == 2) ev_prep = w.ready_host ? nullptr : w.ready;
     // ---- the two sweeps, enqueued interleaved so that the GPU starts on the
     // pooling chain as soon as the first fits are done:
     //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
@@ -4544,7 +4579,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         return FARMS_OK;
     };
-    HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
+    if (ev_prep) HIPCHK(hipStreamWaitEvent(sc, ev_prep, 0));
     hipEvent_t t_pool0 = nullptr;  // the pooling sweep's start: the chain stream past the prep (phase 2: the fits)
     if (prof && phase != 1) { int rc = mark(h, sc, &t_pool0); if (rc) return rc; }
     // the candidate build of the call (k_cand / k_chain), decided on the host
@@ -4579,6 +4614,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             h->brk.push_back({t_prep, e2, kBrFitSweep});
         }
         HIPCHK(hipEventRecord(w.ready, s));
+        w.ready_host = false;
         if (!async) HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipGetLastError());
         h->acc.n_events += n;  // counted here; the pooling call (phase 2) counts its pooling work
@@ -5110,6 +5146,7 @@ extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t
                            d_idx, (int)count, d_flows);
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
+    h->ws[f.set].ready_host = true;  // F drained: the fits of this phase are done
     return FARMS_OK;
 }
 
@@ -5128,6 +5165,7 @@ extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t
     HIPCHK(hipEventRecord(w.ready, h->stream));  // the pooling of this fit waits for its imports
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
+    w.ready_host = true;
     return FARMS_OK;
 }
 

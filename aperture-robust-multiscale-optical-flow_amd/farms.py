@@ -85,6 +85,8 @@ class FarmsStats(ctypes.Structure):
         ("n_owned", ctypes.c_int64),
         ("ms_fit_busy", ctypes.c_double),
         ("ms_pool_busy", ctypes.c_double),
+        ("pool_scan_max", ctypes.c_int64),
+        ("pool_scan_over_1k", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

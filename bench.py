@@ -495,7 +495,9 @@ def main():
                    "profiling": f"{args.prof}, {max(args.prof_steps, 1)} steps after the timed ones",
                    "dense_equiv_bytes_per_event": round(20.0 * cs["pool_cells"] / max(n_owned, 1), 1),
                    "cand_per_valid": round(cs["pool_candidates"] / max(cs["n_valid"], 1), 1),
-                   "contrib_per_valid": round(cs["pool_contributors"] / max(cs["n_valid"], 1), 1)},
+                   "contrib_per_valid": round(cs["pool_contributors"] / max(cs["n_valid"], 1), 1),
+                   "cand_max": cs.get("pool_scan_max", 0),
+                   "cand_over_1k_frac": round(cs.get("pool_scan_over_1k", 0) / max(cs["n_valid"], 1), 6)},
     }
     if world == 1 and args.host_steps > 0:
         line["host_path"] = host_path(fm, sh.x, sh.y, sh.t, sh.p, args.host_steps)

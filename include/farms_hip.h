@@ -108,6 +108,9 @@ typedef struct {
      * when the launches never overlap; below it when two fit streams run
      * launches side by side (fs 7), where the sum counts the overlap twice. */
     double ms_fit_busy, ms_pool_busy;
+    /* the tail of the candidates scanned per pooled event (counting on, as
+     * pool_candidates): the largest, and the events scanning more than 1,024 */
+    int64_t pool_scan_max, pool_scan_over_1k;
 } farms_stats;
 
 /* vFlowManager ctor defaults: 320 x 320, filter 3, 5 inliers (main.cpp:21-24),

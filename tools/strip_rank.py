@@ -38,6 +38,8 @@ ap.add_argument("--nsub", type=int, default=8, help="strips: sub-batches of the 
 ap.add_argument("--pool", type=int, default=0, help="pooling chunk (0: the engine's default)")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--split", choices=multirank.SPLITS, default="strips")
+ap.add_argument("--host-times", action="store_true",
+                help="strips: print the host time of each call of the last timed step (where the host blocks)")
 ap.add_argument("--halo-cache", default="",
                 help="strips: directory of the halo flows per rank (.npy); computed and saved when absent, "
                      "loaded when present, so that a profiled run (rocprofv3 --pmc) holds only the rank's own "
@@ -106,25 +108,34 @@ for r in ranks:
         sae = torch.empty(W * H, dtype=torch.int64, device=dev)
         o = sh.seg.n_warm
 
+    log = []
+
+    def timed(tag, fn, *args):
+        t = time.perf_counter()
+        fn(*args)
+        log.append((tag, t, time.perf_counter()))
+
     def run():
         fm.reset()
+        log.clear()
         if sh.lists is not None:
             # the order of multirank.Stepper.step: fit b+1, pool b, then the
             # exchange of b+1 (its export waits for the fit; import)
             def fit(b):
                 lo, hi, _, _ = subs[b]
-                fm.fit_device(dx[lo:hi], dy[lo:hi], dt[lo:hi], dp[lo:hi], {c: v[lo:hi] for c, v in out.items()})
+                timed(f"fit{b}", fm.fit_device, dx[lo:hi], dy[lo:hi], dt[lo:hi], dp[lo:hi],
+                      {c: v[lo:hi] for c, v in out.items()})
 
             def exchange(b):
                 _, _, hi_idx, hf = subs[b]
-                fm.export_flows(hi_idx[:1], ex_buf)
-                fm.import_flows(hi_idx, hf)
+                timed(f"export{b}", fm.export_flows, hi_idx[:1], ex_buf)
+                timed(f"import{b}", fm.import_flows, hi_idx, hf)
             fit(0)
             exchange(0)
             for b in range(len(subs)):
                 if b + 1 < len(subs):
                     fit(b + 1)
-                fm.pool_device()
+                timed(f"pool{b}", fm.pool_device)
                 if b + 1 < len(subs):
                     exchange(b + 1)
             return
@@ -142,6 +153,11 @@ for r in ranks:
         run()
         torch.cuda.synchronize()
         best = min(best, time.perf_counter() - t1)
+    if a.host_times and log:
+        z = log[0][1]
+        print("host calls of the last step (ms from its start: begin, duration):", flush=True)
+        for tag, t0c, t1c in log:
+            print(f"  {tag:10s} {1e3 * (t0c - z):8.2f} {1e3 * (t1c - t0c):8.2f}", flush=True)
     fm.close()
     worst = max(worst, best)
     print(json.dumps({"n": a.n, "rank": r, "split": a.split, "config": a.config, "nsub": a.nsub,

@@ -258,6 +258,12 @@ struct Ctx {
     int *cinfo;
     int32_t *cscr;         // k_cand scratch: per chunk of a launch, WH item slots (a band's at its first cell)
     const int32_t *bstart; // k_cand: per pooling chunk, the work-order start of each column band (nbands + 1)
+    // k_cand's S2 sources (k_cand_export): per pooling chunk, its events that
+    // are the last at their cell in the chunk with a valid flow, {event, cell,
+    // stamp, next event at the cell}, compacted in work order at the chunk's
+    // first position, and each column band's start in that list (nbands + 1)
+    int4 *s2x;
+    int32_t *s2b;
     int nbands, bandc;     // column bands, columns per band (bandc * H: whole candidate groups)
     int tilesH, tshift;    // work-order tiles per column, log2 of the tile edge
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
@@ -1936,6 +1942,12 @@ __global__ __launch_bounds__(256) void k_fit_wave(Ctx c, uint32_t seq, const int
 // at C3 (round 3): 128 cells (78 VGPRs, 6 waves; or 64 VGPRs, 8 waves) 92-95 ms
 // per step, 512 cells (229 VGPRs, 2 waves) 95 ms, against 87.5 for 256: more
 // chain waves take slots from the fit and pooling, fewer lengthen the chain.
+// acc + the set bits of m below this lane (v_mbcnt_lo / v_mbcnt_hi: two VALU
+// in place of a mask, two ANDs and two bit counts)
+__device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)acc));
+}
+
 constexpr int kGroupCells = 256;
 
 // The call's candidate-build plan (Ctx::cinfo, per workspace set):
@@ -1995,7 +2007,6 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
     if (g >= c.nblk) return;
     const int n = c.n, C2 = c.C2;
     const int lim = min(ch1 * C2, n);  // local flows of events < lim are final
-    const uint64_t lt = (1ull << lane) - 1;
     int k[kChainCells], kend[kChainCells], nxt[kChainCells], pnx[kChainCells];
     ChainFlow snap[kChainCells], pf[kChainCells];
     uint32_t dirty = 0;
@@ -2110,7 +2121,7 @@ __global__ __launch_bounds__(64, FARMS_CHAIN_WAVES) void k_chain(Ctx c, int ch0,
                     v.L1 = 0.0; v.Lc1 = 0.0; v.Ls1 = 0.0;
                     v.run_lo = 0; v.run_hi = 0;
                 }
-                const int64_t kb = (int64_t)b * c.cstride + woff[i] + (uint32_t)__popcll(bal[i] & lt);
+                const int64_t kb = (int64_t)b * c.cstride + (uint32_t)mbcnt64(bal[i], (int)woff[i]);
                 c.hdr_ring[kb] = hd;
                 c.val_ring[kb] = v;
             }
@@ -2345,6 +2356,60 @@ __global__ void k_band_starts(Ctx c, const uint32_t *wkey_sorted, int tile_bits,
         for (int b = bw + 1; b <= c.nbands; ++b) bs[b] = ce;
 }
 
+// k_cand's S2 sources of pooling chunks [ch0, ch1), one 256-thread block per
+// chunk (round 5): an event of chunk cp can be an S2 candidate of a later
+// chunk ch only if it is the last event at its cell before ch's end -- so the
+// last at its cell in cp (next event at or past cp's end) -- and its flow is
+// valid.  Those events, compacted in work order (band-ascending), with the
+// start of each column band in the list: a later chunk's S2 reads 16 B per
+// such event of its band, where it read every event's descriptor, link and
+// flow of each of the ~3 chunks its kill window reaches (C3: most of k_cand's
+// HBM traffic).  Runs on the chain stream after the super-chunk's flows
+// (k_flow; the imports of an x-strip call) and before its k_cand.
+__global__ __launch_bounds__(256) void k_cand_export(Ctx c, int ch0, int ch1) {
+    __shared__ int s_wsum[4];
+    const int ch = ch0 + (int)blockIdx.x;
+    if (ch >= ch1) return;
+    const int cs = ch * c.C2, ce = min(cs + c.C2, c.n);
+    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int H = c.H, OFF = c.X0 * H;
+    int32_t *bs = c.s2b + (int64_t)ch * (c.nbands + 1);
+    auto band_of = [&](int x) { return (x - c.X0) / c.bandc; };
+    int carry = 0;
+    for (int base = cs; base < ce; base += 256) {
+        const int w = base + tid;
+        bool keep = false;
+        int4 rec = make_int4(0, 0, 0, 0);
+        int b = 0, bp = -1;
+        if (w < ce) {
+            const int4 fd = c.fdesc[w];  // {event, x, y, t}
+            b = band_of(fd.y);
+            if (w > cs) bp = band_of(c.fdesc[w - 1].y);
+            const int nx = c.link[fd.x].z;
+            if (nx >= ce && c.evf[fd.x].L > 0) {
+                keep = true;
+                rec = make_int4(fd.x, fd.y * H + fd.z - OFF, fd.w, nx);
+            }
+        }
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) s_wsum[wv] = (int)__popcll(bal);
+        __syncthreads();
+        int off = carry;
+        for (int i = 0; i < wv; ++i) off += s_wsum[i];
+        const int tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+        const int rank = mbcnt64(bal, off);  // kept events before w in the chunk
+        if (keep) c.s2x[cs + rank] = rec;
+        if (w < ce)
+            for (int q = bp + 1; q <= b; ++q) bs[q] = rank;  // the bands that start at w
+        __syncthreads();  // (s_wsum is rewritten next round)
+        carry += tot;
+    }
+    if (tid == 0) {  // bands past the last event's: the list's end
+        const int bl = band_of(c.fdesc[ce - 1].y);
+        for (int q = bl + 1; q <= c.nbands; ++q) bs[q] = carry;
+    }
+}
+
 // One wavefront (= one workgroup: it slots in as the pooling waves free theirs)
 // per (pooling chunk, band of columns) of chunks [ch0, ch1).  A band's cells
 // [b * bandc * H, ...) start on a candidate-group boundary (bandc * H is a
@@ -2369,14 +2434,13 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
     const int64_t lo = (int64_t)c.ctmin[ch] - (int64_t)kKillUs, hi = (int64_t)c.ctmax[ch] + (int64_t)kKillUs;
     const int cap = (int)(qb - qa);
     int32_t *scr = c.cscr + (int64_t)(ch - ch0) * c.WH + qa;  // this band's item slots in the chunk's scratch
-    const uint64_t lt = (1ull << lane) - 1;
     const int OFF = c.X0 * H;
     int cnt = 0;  // (wave-uniform)
     auto push = [&](bool keep, uint32_t q, int item) {
         const uint64_t bal = __ballot(keep);
         if (keep) {
             atomicOr((unsigned long long *)&s_bm[(q - qa) >> 6], 1ull << (q & 63));
-            const int i = cnt + (int)__popcll(bal & lt);
+            const int i = mbcnt64(bal, cnt);
             if (i < cap) scr[i] = item;  // (a cell is an item at most once: i < cap always)
         }
         cnt += (int)__popcll(bal);
@@ -2410,23 +2474,24 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
         }
     }
     // S2: the last events before the chunk at untouched cells, from the chunks
-    // whose stamps reach the kill window
+    // whose stamps reach the kill window: their exported sources (the events
+    // last at their cell in their own chunk with a valid flow, k_cand_export),
+    // 16 B each, in work order -- a superset of this chunk's S2 from them
+    const int32_t *s2r = c.s2b + (int64_t)bd;
     for (int cp = c.cbk[ch]; cp < ch; ++cp) {
         if (!((int64_t)c.ctmax[cp] > lo && (int64_t)c.ctmin[cp] < hi)) continue;
-        const int w0 = bsr[cp * bstride], w1 = bsr[cp * bstride + 1];
-        for (int wb = w0; wb < w1; wb += 64) {
-            const int w = wb + lane;
+        const int x0 = cp * C2 + s2r[cp * bstride], x1 = cp * C2 + s2r[cp * bstride + 1];
+        for (int xb = x0; xb < x1; xb += 64) {
+            const int x = xb + lane;
             bool keep = false;
             uint32_t q = 0;
             int e = 0;
-            if (w < w1) {
-                const int4 fd = c.fdesc[w];
-                const int64_t te = (int64_t)(uint32_t)fd.w;
-                e = fd.x;
-                if (te > lo && te < hi) {
-                    q = (uint32_t)(fd.y * H + fd.z - OFF);
-                    if (c.link[e].z >= ce) keep = c.evf[e].L > 0;
-                }
+            if (x < x1) {
+                const int4 r = c.s2x[x];  // {event, cell, stamp, next event at the cell}
+                const int64_t te = (int64_t)(uint32_t)r.z;
+                e = r.x;
+                q = (uint32_t)r.y;
+                keep = te > lo && te < hi && r.w >= ce;
             }
             push(keep, q, e);
         }
@@ -2786,9 +2851,8 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         const int cnt = n0[hh] + n1[hh];
         const int incl = wave_incl_scan(cnt);
         const int start = carry + incl - cnt;
-        const uint64_t lt = (1ull << lane) - 1;
         const uint64_t b0 = __ballot(n0[hh] > 0), b1 = __ballot(n1[hh] > 0);
-        int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
+        int idx = mbcnt64(b1, mbcnt64(b0, nz));
         if (n0[hh] > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(a0[hh] - start + kRowBias);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
@@ -2861,7 +2925,6 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
     constexpr int NH = kPoolHalves;  // candidates per lane per step: a step covers 64 * NH positions
 #pragma unroll
     for (int i = lane; i < kPoolSlots; i += 64) s_val[4 * i + 3] = 1.0;  // the count's "value" (staging never overwrites it)
-    const uint64_t lt = (1ull << lane) - 1;
     double acc = 0.0;
     int ncon_total = 0;
     // lanes without a contributor load the event's own flow (a valid address,
@@ -2985,7 +3048,7 @@ __device__ __forceinline__ void pool_one(const Ctx &c, int e, int ex, int ey, ui
 #pragma unroll
             for (int h = 0; h < NH; ++h) {
                 if ((pbal[h] >> lane) & 1) {
-                    const int slot = cbase + (int)__popcll(pbal[h] & lt);
+                    const int slot = mbcnt64(pbal[h], cbase);
                     s_val[4 * slot] = pv[h][0]; s_val[4 * slot + 1] = pv[h][1]; s_val[4 * slot + 2] = pv[h][2];
                     s_k0[slot] = (uint8_t)(kenc_mul * pk0[h]);
                 }
@@ -3194,7 +3257,13 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
 // event per step; the events of a pair are consecutive pooled events of one
 // pooling chunk in work order (k_pool_compact), so their windows overlap and
 // their step counts match.
-constexpr int kPairSlots = 40;  // staged entries per event: <= 32 per step + < 8 carried
+// FARMS_PAIR_RING=1 (tuning build): the staged entries in a 64-slot ring per
+// event, read in groups of 8 from a moving read pointer, so that the rest of
+// each step (< 8 entries) stays in place instead of being copied to the front
+#ifndef FARMS_PAIR_RING
+#define FARMS_PAIR_RING 0
+#endif
+constexpr int kPairSlots = FARMS_PAIR_RING ? 64 : 40;  // staged entries per event: <= 32 per step + < 8 carried
 template <int K>
 constexpr bool kPairPool = K >= 2 && K <= 11;
 constexpr uint32_t kPairJunk = 0x1E1E1E1Eu;  // four shift bytes of 30: the half's lanes 30, 31 only
@@ -3223,7 +3292,6 @@ __global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, i
     if (ch >= ch1) return;
     const int cs = ch * c.C2, ce = min(cs + c.C2, c.n);
     const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint64_t lt = (1ull << lane) - 1;
     int carry = 0;
     for (int base = cs; base < ce; base += 256) {
         const int w = base + tid;
@@ -3239,7 +3307,7 @@ __global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, i
         int off = carry;
         for (int i = 0; i < wv; ++i) off += s_wsum[i];
         const int tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-        if (ok) c.qe[cs + off + (int)__popcll(bal & lt)] = fd;
+        if (ok) c.qe[mbcnt64(bal, cs + off)] = fd;
         __syncthreads();  // (s_wsum is rewritten next round)
         carry += tot;
     }
@@ -3298,10 +3366,11 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
     bool has_[NB], str_[NB];
     uint64_t bA[NB], bB[NB], bC[NB];
     uint32_t oA[NB], oB[NB], oC[NB];
+    const int base0 = (i_lo + hl) * H;  // (rows past the window: addresses clamped below, has_ false)
 #pragma unroll
     for (int hh = 0; hh < NB; ++hh) {
         const int r = hl + 32 * hh;
-        const int base = (i_lo + (r < nrows ? r : 0)) * H;
+        const int base = base0 + 32 * hh * H;
         int l1 = base + j_hi;
         if (l1 > WHs - 1) l1 = WHs - 1;  // past the end of the sensor: no contribution
         int l0 = base + j_lo - OFF;
@@ -3322,7 +3391,6 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         bC[hh] = C.bm; oC[hh] = C.wo;
     }
     int carry = 0, nz = 0;
-    const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
     for (int hh = 0; hh < NB; ++hh) {
         const int r = hl + 32 * hh;
@@ -3335,7 +3403,7 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         const int incl = half_incl_scan(cnt);
         const int start = carry + incl - cnt;
         const uint64_t b0 = __ballot(n0 > 0) & hm, b1 = __ballot(n1 > 0) & hm;
-        int idx = nz + (int)__popcll(b0 & lt) + (int)__popcll(b1 & lt);
+        int idx = mbcnt64(b1, mbcnt64(b0, nz));
         if (n0 > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
             if (FARMS_PAIR_BITCAP == 0 || start < FARMS_PAIR_BITCAP) atomicOr(&sbits[start >> 5], 1u << (start & 31));
@@ -3397,7 +3465,6 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     const int OFF = c.X0 * c.H;
     const int hl = lane & 31;
     const uint64_t hm = lane < 32 ? 0x00000000FFFFFFFFull : 0xFFFFFFFF00000000ull;
-    const uint64_t lt = (1ull << lane) - 1;
     // serial mode: the own cell is pooled with the stamp its lastEventTime
     // still holds (vFlow.cpp:790 vs :264)
     const uint32_t own_lin = c.serial ? (uint32_t)((ex - c.X0) * H + ey) : 0xFFFFFFFFu;
@@ -3439,6 +3506,9 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     double pv0 = 0.0, pv1 = 0.0, pv2 = 0.0;
     int pk0 = K;
     int stA = 0, stB = 0;  // (wave-uniform) staged entries not yet folded, per event
+#if FARMS_PAIR_RING
+    int rdA = 0, rdB = 0;  // (wave-uniform) ring slot of the first of them (a multiple of 8)
+#endif
     for (int f0 = 0;; f0 += 32) {
         const bool have = f0 < tmax;  // wave-uniform
         bool con = false;
@@ -3487,7 +3557,11 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if ((pbal >> lane) & 1) {
-                const int slot = (lane < 32 ? stA : stB) + (int)__popcll(pbal & lt & hm);
+#if FARMS_PAIR_RING
+                const int slot = mbcnt64(pbal & hm, lane < 32 ? rdA + stA : rdB + stB) & (kPairSlots - 1);
+#else
+                const int slot = mbcnt64(pbal & hm, lane < 32 ? stA : stB);
+#endif
                 s_val[3 * slot] = pv0; s_val[3 * slot + 1] = pv1; s_val[3 * slot + 2] = pv2;
                 s_k0[slot] = (uint8_t)(pk0 > 0 ? 3 * (pk0 - 1) : 0);
                 atomicAdd(&s_hist[pk0], 1);
@@ -3501,19 +3575,29 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
             const int wA = stA & ~7, wB = stB & ~7;
             const int wmaxg = wA > wB ? wA : wB;
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
+#if FARMS_PAIR_RING
+            const int rd_h = lane < 32 ? rdA : rdB;
+#else
+            constexpr int rd_h = 0;
+#endif
 #pragma unroll 1
             for (int r = 0; r < wmaxg; r += 8) {
-                const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
+                const int g = (rd_h + r) & (FARMS_PAIR_RING ? kPairSlots - 1 : 0x7FFFFFFF);
+                const uint32_t kw0 = k4p[g >> 2], kw1 = k4p[(g >> 2) + 1];
                 double vv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (r + u) + q];
+                for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (g + u) + q];
                 const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
                 const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
                 fold8_pair(acc, r < wA ? a0 : kPairJunk, r < wA ? a1 : kPairJunk, r < wB ? b0 : kPairJunk,
                            r < wB ? b1 : kPairJunk, vv);
             }
-            // carry each event's rest (< 8) to its slots [0, rest)
             const int rA = stA - wA, rB = stB - wB;
+#if FARMS_PAIR_RING
+            rdA = (rdA + wA) & (kPairSlots - 1);
+            rdB = (rdB + wB) & (kPairSlots - 1);
+#else
+            // carry each event's rest (< 8) to its slots [0, rest)
             const int w_h = lane < 32 ? wA : wB, r_h = lane < 32 ? rA : rB;
             if ((wA > 0 && rA > 0) || (wB > 0 && rB > 0)) {
                 double m0 = 0.0, m1 = 0.0, m2 = 0.0;
@@ -3530,6 +3614,7 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
                     s_k0[hl] = mk;
                 }
             }
+#endif
             stA = rA;
             stB = rB;
         }
@@ -3543,14 +3628,19 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int st_h = lane < 32 ? stA : stB;
-        if (hl >= st_h && hl < 8) s_k0[hl] = (uint8_t)30;
+#if FARMS_PAIR_RING
+        const int g = lane < 32 ? rdA : rdB;
+#else
+        constexpr int g = 0;
+#endif
+        if (hl >= st_h && hl < 8) s_k0[g + hl] = (uint8_t)30;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
-        const uint32_t kw0 = k4p[0], kw1 = k4p[1];
+        const uint32_t kw0 = k4p[g >> 2], kw1 = k4p[(g >> 2) + 1];
         double vv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * u + q];
+        for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (g + u) + q];
         const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
         const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
         fold8_pair(acc, stA > 0 ? a0 : kPairJunk, stA > 0 ? a1 : kPairJunk, stB > 0 ? b0 : kPairJunk,
@@ -3563,9 +3653,10 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     // lane 3 (k - 1) + q's sums; counts from the histogram (exact integers)
     const int base = lane & 32;
     const int kl = hl < K ? hl : 0;
-    int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) cnt += k <= kl ? s_hist[k] : 0;
+    // counts per scale: the histogram's prefix sums over the half's lanes
+    // (lane hl < K: contributors with smallest scale <= hl)
+    const int pref = half_incl_scan(hl < K ? s_hist[hl] : 0);
+    const int cnt = pref;
     const bool own_ok = s_own[3] != 0.0;
     const double len_k = __shfl(acc, base + 3 * (kl > 0 ? kl - 1 : 0), 64);
     const double L_k = kl == 0 ? (own_ok ? s_own[0] : 0.0) : len_k;
@@ -3574,9 +3665,8 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     const double maxv = half_max(mean);
     const uint64_t win = __ballot(is_len && mean == maxv) & hm;
     const int mi = maxv > 0 ? (int)__builtin_ctzll(win) - base : 0;
-    int cnt_mi = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) cnt_mi += k <= mi ? s_hist[k] : 0;
+    const int miA = __builtin_amdgcn_readlane(mi, 0), miB = __builtin_amdgcn_readlane(mi, 32);
+    const int cnt_mi = lane < 32 ? __builtin_amdgcn_readlane(pref, miA) : __builtin_amdgcn_readlane(pref, 32 + miB);
     const int src = base + 3 * (mi > 0 ? mi - 1 : 0);
     const double sx_s = __shfl(acc, src + 1, 64), sy_s = __shfl(acc, src + 2, 64);
     const double sx = mi == 0 ? s_own[1] : sx_s, sy = mi == 0 ? s_own[2] : sy_s;
@@ -3602,7 +3692,7 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
 // chunk ch takes its compacted events 2p and 2p + 1 (k_pool_compact); pairs
 // past the chunk's count leave at once.  Same occupancy cap as k_pool.
 template <int K, bool W7>
-__global__ __launch_bounds__(64) void k_pool2(Ctx c, int ch0, int ch1, const int32_t *nv) {
+__global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch1, const int32_t *nv) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
     else asm volatile("" ::: FARMS_POOL_FLOOR_6);
@@ -3816,6 +3906,8 @@ struct Work {
     int32_t *cbk = nullptr;                    // k_cand plan: first chunk reaching each chunk's kill window
     int32_t *bstart = nullptr;                 // k_cand: per chunk, the work-order start of each column band
     int32_t *nv = nullptr;                     // paired pooling: per chunk, its pooled events (k_pool_compact)
+    int4 *s2x = nullptr;                       // k_cand_export: per chunk, its S2 sources
+    int32_t *s2b = nullptr;                    // ... and their column bands' starts
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
     int32_t *pcur = nullptr, *pend = nullptr;  // per cell: the call's pooling-chain cursor / last run position
@@ -3938,7 +4030,7 @@ void free_workspace(Work &w) {
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
-    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart); dfree(w.nv);
+    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart); dfree(w.nv); dfree(w.s2x); dfree(w.s2b);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -3971,7 +4063,8 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         (rc = dalloc(&w.plane, cap)) || (rc = dalloc(&w.wkey, cap)) || (rc = dalloc(&w.wkey_sorted, cap)) ||
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
         (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch)) || (rc = dalloc(&w.cpmax, nch)) ||
-        (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1))) || (rc = dalloc(&w.nv, nch))) {
+        (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1))) || (rc = dalloc(&w.nv, nch)) ||
+        (rc = dalloc(&w.s2x, cap)) || (rc = dalloc(&w.s2b, nch * (h->nbands + 1)))) {
         free_workspace(w);
         return rc;
     }
@@ -4288,6 +4381,7 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.pcur = w.pcur; c.pend = w.pend;
     c.cbk = w.cbk; c.slist = w.slist; c.cinfo = w.cinfo; c.cscr = h->cscr;
     c.bstart = w.bstart; c.nbands = h->nbands; c.bandc = h->bandc;
+    c.s2x = w.s2x; c.s2b = w.s2b;
     c.tshift = h->tile_shift; c.tilesH = (h->H + (1 << h->tile_shift) - 1) >> h->tile_shift;
     c.serial = h->prm.serial != 0;
     c.bw_ring = h->bw_ring; c.nblk = h->nblk; c.cstride = h->cstride;
@@ -4644,6 +4738,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 64)), dim3(64), 0, sc, c, q0, q1);
         }
         if (use_cand < 0) { int rc = decide_cand(); if (rc) return rc; }
+        if (use_cand) hipLaunchKernelGGL(k_cand_export, dim3(ch1 - ch0), dim3(256), 0, sc, c, ch0, ch1);
         for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (k_chain: their spans in one VGPR)
             const int b = std::min(a + 64, ch1);
             if (use_cand)

@@ -3345,7 +3345,7 @@ __device__ __forceinline__ double half_max(double v) {
 // hl + 32, hl + 64, hl + 96) into its own LDS arrays; returns the half's
 // flattened length (0 for an absent event).
 __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool act, int i_lo, int nrows, int j_lo,
-                                          int j_hi, uint64_t *s_start, uint32_t *s_row) {
+                                          int j_hi, uint64_t *s_start, uint32_t *s_row, int &nseg) {
     const int H = c.H;
     const int WHl = (int)c.WH, OFF = c.X0 * c.H;
     const int WHs = (int)c.WHs;
@@ -3419,6 +3419,7 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    nseg = nz;
     return carry;
 }
 
@@ -3457,7 +3458,7 @@ template <int K>
 __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int e, int ex, int ey, uint32_t teu,
                                           int buf, int row_i0, int total, int totA, int totB,
                                           const uint64_t *s_start, const uint32_t *s_row, double *s_val,
-                                          uint8_t *s_k0, int *s_hist, double *s_own) {
+                                          uint8_t *s_k0, int *s_hist, double *s_own, int nseg) {
     static_assert(kPairPool<K>, "paired pooling: 3 (K - 1) <= 30 lanes per event");
     const CandHdr *chdr = c.hdr_ring + (int64_t)buf * c.cstride;
     const CandVal *cval = c.val_ring + (int64_t)buf * c.cstride;
@@ -3482,8 +3483,12 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     auto locate = [&](int f0, int &row, int &k) {
         const uint64_t mk = s_start[f0 >> 6];
         const int bit = (f0 & 63) + hl;
-        const int m = mbase + (int)__popcll(mk & ((2ull << bit) - 1)) - 1;
+        int m = mbase + (int)__popcll(mk & ((2ull << bit) - 1)) - 1;
         if ((f0 & 63) == 32) mbase += (int)__popcll(mk);
+        // a half past its window's end (or without an event) reads bitmap
+        // words it never wrote: keep its segment index inside its own table
+        // (its k is replaced by safe_k's anyway)
+        m = m > nseg - 1 ? nseg - 1 : m;
         const uint32_t rs = s_row[m < 0 ? 0 : m];
         row = (int)(rs >> 25);
         k = f0 + hl + (int)(rs & 0x1FFFFFFu) - kRowBias;
@@ -3709,8 +3714,16 @@ __global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch
     if (2 * p >= cnt) return;
     const bool hasB = 2 * p + 1 < cnt;
     const bool act = lane < 32 || hasB;
-    const int4 d = act ? dq : make_int4(__builtin_amdgcn_readfirstlane(dq.x), __builtin_amdgcn_readfirstlane(dq.y),
-                                        __builtin_amdgcn_readfirstlane(dq.z), __builtin_amdgcn_readfirstlane(dq.w));
+    // a half without an event takes event A's fields: lane 0's, by readlane.
+    // (readfirstlane would read the first lane of the exec mask the compiler
+    // evaluates this select under -- lane 32 when only the idle half is
+    // active -- i.e. the stale descriptor past the chunk's count: an event id
+    // from an earlier call or handle, whose flow the idle lanes then loaded.
+    // Freshly mapped memory holds zeros, so it showed only after another
+    // call or handle had used the memory: the strip steps and a test sequence
+    // faulted, round 5.)
+    const int4 d = act ? dq : make_int4(__builtin_amdgcn_readlane(dq.x, 0), __builtin_amdgcn_readlane(dq.y, 0),
+                                        __builtin_amdgcn_readlane(dq.z, 0), __builtin_amdgcn_readlane(dq.w, 0));
     const int e = d.x, ex = d.y, ey = d.z;
     const uint32_t teu = (uint32_t)d.w;
     const int buf = (c.ring0 + ch) % c.NB;  // the pair's chunk's candidate buffer
@@ -3726,11 +3739,12 @@ __global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    int nseg;
+    int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
     if (FARMS_PAIR_BITCAP > 0 && total > FARMS_PAIR_BITCAP - 64) total = 0;  // (experiment: skipped)
     const int totA = __builtin_amdgcn_readlane(total, 0), totB = __builtin_amdgcn_readlane(total, 32);
     pool_pair<K>(c, lane, act, e, ex, ey, teu, buf, i_lo, total, totA, totB, s_start, s_row, s_val, s_k0, s_hist,
-                 s_own);
+                 s_own, nseg);
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -4429,7 +4443,13 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     const int n_pool_chunks = ceil_div(n, h->pool_chunk);
     const uint32_t *dt = c.t;
     hipEvent_t ev_prep = w.sync_ev[0];
-    if (!validated) {  // on the copy stream (idle in device calls): no wait behind F
+    if (!validated) {
+        // on the copy stream: not behind F's work.  In device calls that stream
+        // also runs the odd fit chunks (fs 7), so the host waits for the
+        // previous call's odd fits here -- in the x-strip pipeline those are
+        // already done (the exchange's export synchronized F behind them):
+        // farms_fit_device returns in 1.1-1.3 ms of host time there
+        // (profiles/r05_strip_host_times.log)
         hipStream_t sv = h->s_copy;
         int herr = 0;
         HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), sv));

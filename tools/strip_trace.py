@@ -63,12 +63,16 @@ def main():
     for r in csv.DictReader(open(a.csv)):
         m = re.search(r"(k_\w+)", r["Kernel_Name"])
         name = m.group(1) if m else r["Kernel_Name"][:40]
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r.get("Stream_Id", "")))
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r.get("Stream_Id", ""),
+                     r.get("Queue_Id", "")))
     rows.sort()
     preps = [i for i, r in enumerate(rows) if r[2] == "k_prep"]
     per = a.preps or (8 if len(preps) >= 16 else 1)
     lo = preps[len(preps) - per]
-    sel = [r for r in rows[lo:] if r[2] != "k_stats"]
+    queues = collections.defaultdict(set)  # the hardware queue(s) each stream's kernels went through
+    for r in rows:
+        queues[r[3]].add(r[4])
+    sel = [r[:4] for r in rows[lo:] if r[2] != "k_stats"]
     t0, t1 = sel[0][0], max(r[1] for r in sel)
     span = t1 - t0
     busy = union([(s, e) for s, e, *_ in sel])
@@ -93,7 +97,8 @@ def main():
     print("streams:")
     for st, iv in sorted(streams.items()):
         ks = collections.Counter(k for _, _, k in iv)
-        print(f"  stream {st}: busy {union([(s, e) for s, e, _ in iv]) / 1e6:8.2f} ms  {dict(ks.most_common(4))}")
+        print(f"  stream {st} (queue {','.join(sorted(queues[st]))}): busy {union([(s, e) for s, e, _ in iv]) / 1e6:8.2f} ms"
+              f"  {dict(ks.most_common(4))}")
     if a.timeline:
         nb = int(span // 2_000_000) + 1
         print("timeline (2-ms bins, busy fraction per stream: " + " ".join(sorted(streams)) + ")")

@@ -258,10 +258,11 @@ struct Ctx {
     int *cinfo;
     int32_t *cscr;         // k_cand scratch: per chunk of a launch, WH item slots (a band's at its first cell)
     const int32_t *bstart; // k_cand: per pooling chunk, the work-order start of each column band (nbands + 1)
-    // k_cand's S2 sources (k_cand_export): per pooling chunk, its events that
-    // are the last at their cell in the chunk with a valid flow, {event, cell,
-    // stamp, next event at the cell}, compacted in work order at the chunk's
-    // first position, and each column band's start in that list (nbands + 1)
+    // k_cand's S2 sources (k_cand_export): per (pooling chunk, column band),
+    // its events that are the last at their cell in the chunk with a valid
+    // flow, {event, cell, stamp, next event at the cell}, compacted to the
+    // front of the band's work-order range, and their number (s2b, at the
+    // band's bstart index)
     int4 *s2x;
     int32_t *s2b;
     int nbands, bandc;     // column bands, columns per band (bandc * H: whole candidate groups)
@@ -2356,35 +2357,33 @@ __global__ void k_band_starts(Ctx c, const uint32_t *wkey_sorted, int tile_bits,
         for (int b = bw + 1; b <= c.nbands; ++b) bs[b] = ce;
 }
 
-// k_cand's S2 sources of pooling chunks [ch0, ch1), one 256-thread block per
-// chunk (round 5): an event of chunk cp can be an S2 candidate of a later
-// chunk ch only if it is the last event at its cell before ch's end -- so the
-// last at its cell in cp (next event at or past cp's end) -- and its flow is
-// valid.  Those events, compacted in work order (band-ascending), with the
-// start of each column band in the list: a later chunk's S2 reads 16 B per
-// such event of its band, where it read every event's descriptor, link and
-// flow of each of the ~3 chunks its kill window reaches (C3: most of k_cand's
-// HBM traffic).  Runs on the chain stream after the super-chunk's flows
-// (k_flow; the imports of an x-strip call) and before its k_cand.
-__global__ __launch_bounds__(256) void k_cand_export(Ctx c, int ch0, int ch1) {
-    __shared__ int s_wsum[4];
-    const int ch = ch0 + (int)blockIdx.x;
+// k_cand's S2 sources of pooling chunks [ch0, ch1) (round 5): an event of
+// chunk cp can be an S2 candidate of a later chunk ch only if it is the last
+// event at its cell before ch's end -- so the last at its cell in cp (next
+// event at or past cp's end) -- and its flow is valid.  One wavefront per
+// (chunk, column band), as k_cand: the band's such events, compacted in work
+// order to the front of the band's own work-order range {event, cell, stamp,
+// next event}, and their number.  A later chunk's S2 then reads 16 B per such
+// event of its band, where it read every event's descriptor, link and flow of
+// each of the ~3 chunks its kill window reaches.  Runs on the chain stream
+// after the super-chunk's flows (k_flow; the imports of an x-strip call) and
+// before its k_cand.
+__global__ __launch_bounds__(64) void k_cand_export(Ctx c, int ch0, int ch1) {
+    const int lb = work_block();
+    const int ch = ch0 + lb / c.nbands, bd = lb % c.nbands;
     if (ch >= ch1) return;
+    const int lane = (int)threadIdx.x;
     const int cs = ch * c.C2, ce = min(cs + c.C2, c.n);
-    const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int H = c.H, OFF = c.X0 * H;
-    int32_t *bs = c.s2b + (int64_t)ch * (c.nbands + 1);
-    auto band_of = [&](int x) { return (x - c.X0) / c.bandc; };
-    int carry = 0;
-    for (int base = cs; base < ce; base += 256) {
-        const int w = base + tid;
+    const int64_t bi = (int64_t)ch * (c.nbands + 1) + bd;
+    const int w0 = c.bstart[bi], w1 = c.bstart[bi + 1];
+    int cnt = 0;  // (wave-uniform)
+    for (int wb = w0; wb < w1; wb += 64) {
+        const int w = wb + lane;
         bool keep = false;
         int4 rec = make_int4(0, 0, 0, 0);
-        int b = 0, bp = -1;
-        if (w < ce) {
+        if (w < w1) {
             const int4 fd = c.fdesc[w];  // {event, x, y, t}
-            b = band_of(fd.y);
-            if (w > cs) bp = band_of(c.fdesc[w - 1].y);
             const int nx = c.link[fd.x].z;
             if (nx >= ce && c.evf[fd.x].L > 0) {
                 keep = true;
@@ -2392,22 +2391,10 @@ __global__ __launch_bounds__(256) void k_cand_export(Ctx c, int ch0, int ch1) {
             }
         }
         const uint64_t bal = __ballot(keep);
-        if (lane == 0) s_wsum[wv] = (int)__popcll(bal);
-        __syncthreads();
-        int off = carry;
-        for (int i = 0; i < wv; ++i) off += s_wsum[i];
-        const int tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-        const int rank = mbcnt64(bal, off);  // kept events before w in the chunk
-        if (keep) c.s2x[cs + rank] = rec;
-        if (w < ce)
-            for (int q = bp + 1; q <= b; ++q) bs[q] = rank;  // the bands that start at w
-        __syncthreads();  // (s_wsum is rewritten next round)
-        carry += tot;
+        if (keep) c.s2x[w0 + mbcnt64(bal, cnt)] = rec;
+        cnt += (int)__popcll(bal);
     }
-    if (tid == 0) {  // bands past the last event's: the list's end
-        const int bl = band_of(c.fdesc[ce - 1].y);
-        for (int q = bl + 1; q <= c.nbands; ++q) bs[q] = carry;
-    }
+    if (lane == 0) c.s2b[bi] = cnt;
 }
 
 // One wavefront (= one workgroup: it slots in as the pooling waves free theirs)
@@ -2477,10 +2464,9 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
     // whose stamps reach the kill window: their exported sources (the events
     // last at their cell in their own chunk with a valid flow, k_cand_export),
     // 16 B each, in work order -- a superset of this chunk's S2 from them
-    const int32_t *s2r = c.s2b + (int64_t)bd;
     for (int cp = c.cbk[ch]; cp < ch; ++cp) {
         if (!((int64_t)c.ctmax[cp] > lo && (int64_t)c.ctmin[cp] < hi)) continue;
-        const int x0 = cp * C2 + s2r[cp * bstride], x1 = cp * C2 + s2r[cp * bstride + 1];
+        const int x0 = bsr[cp * bstride], x1 = x0 + c.s2b[cp * bstride + bd];
         for (int xb = x0; xb < x1; xb += 64) {
             const int x = xb + lane;
             bool keep = false;
@@ -3257,13 +3243,9 @@ __global__ __launch_bounds__(64) void k_pool(Ctx c, int c0, int c1) {
 // event per step; the events of a pair are consecutive pooled events of one
 // pooling chunk in work order (k_pool_compact), so their windows overlap and
 // their step counts match.
-// FARMS_PAIR_RING=1 (tuning build): the staged entries in a 64-slot ring per
-// event, read in groups of 8 from a moving read pointer, so that the rest of
-// each step (< 8 entries) stays in place instead of being copied to the front
-#ifndef FARMS_PAIR_RING
-#define FARMS_PAIR_RING 0
-#endif
-constexpr int kPairSlots = FARMS_PAIR_RING ? 64 : 40;  // staged entries per event: <= 32 per step + < 8 carried
+// (a 64-slot ring per event instead, read from a moving pointer so that a
+// step's rest stays in place: C3 74.0 against 72.0 ms, profiles/r05_ab_s2.log)
+constexpr int kPairSlots = 40;  // staged entries per event: <= 32 per step + < 8 carried
 template <int K>
 constexpr bool kPairPool = K >= 2 && K <= 11;
 constexpr uint32_t kPairJunk = 0x1E1E1E1Eu;  // four shift bytes of 30: the half's lanes 30, 31 only
@@ -3273,23 +3255,23 @@ constexpr uint32_t kPairJunk = 0x1E1E1E1Eu;  // four shift bytes of 30: the half
 __host__ __device__ constexpr int pair_half_words(int bw, int rs) {
     return bw + rs + 3 * kPairSlots + kPairSlots / 8 + 8 /* hist: 16 ints */ + 4 /* own: L, Lc, Ls, flag */;
 }
-// Timing experiment only (FARMS_PAIR_BITCAP=T builds, never the product): the
-// segment-start bitmap sized for T flattened positions; a wider window's event
-// is skipped (wrong records), to measure what the LDS saved buys.
-#ifndef FARMS_PAIR_BITCAP
-#define FARMS_PAIR_BITCAP 0
-#endif
-__host__ __device__ constexpr int pair_bw(int bw) {
-    return FARMS_PAIR_BITCAP > 0 && bw > FARMS_PAIR_BITCAP / 64 + 1 ? FARMS_PAIR_BITCAP / 64 + 1 : bw;
-}
+// The pair bitmap marks segment starts over the first kPairBitPos flattened
+// window positions only (17 words instead of 161 at maxWindow 50: 4.1 KB of
+// LDS per wave instead of 6.4, C3 72.2 -> 70.0 ms per step on the timing
+// build, profiles/r05_ab_s3.log).  An event whose window holds more candidates
+// (none at C3: at most 899, the scan-width tail of the bench line) is pooled
+// by k_pool_ovf after the launch, one event per wave with the full bitmap.
+constexpr int kPairBitPos = 1024;
+__host__ __device__ constexpr int pair_bw(int bw) { return bw > kPairBitPos / 64 + 1 ? kPairBitPos / 64 + 1 : bw; }
 
 // Ordered compaction of each pooling chunk's pooled events (valid flow, owned
 // column) to the front of its work-order positions: qe[cs + r] = the r-th one's
 // {event, x, y, t}, nv[ch] = their number.  One 256-thread block per chunk.
-__global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, int32_t *nv) {
+__global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, int32_t *nv, int *ovfn) {
     __shared__ int s_wsum[4];
     const int ch = ch0 + (int)blockIdx.x;
     if (ch >= ch1) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ovfn = 0;  // the launch's overflow list starts empty
     const int cs = ch * c.C2, ce = min(cs + c.C2, c.n);
     const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int carry = 0;
@@ -3354,7 +3336,7 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
     uint32_t *const sbits = reinterpret_cast<uint32_t *>(s_start);
     {
         int nw = act ? ((nrows * (j_hi - j_lo + 1) + 63) >> 6) + 1 : 0;
-        if (FARMS_PAIR_BITCAP > 0 && nw > FARMS_PAIR_BITCAP / 64 + 1) nw = FARMS_PAIR_BITCAP / 64 + 1;
+        if (nw > kPairBitPos / 64 + 1) nw = kPairBitPos / 64 + 1;
         for (int i = hl; i < nw; i += 32) s_start[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -3406,12 +3388,12 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         int idx = mbcnt64(b1, mbcnt64(b0, nz));
         if (n0 > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
-            if (FARMS_PAIR_BITCAP == 0 || start < FARMS_PAIR_BITCAP) atomicOr(&sbits[start >> 5], 1u << (start & 31));
+            if (start < kPairBitPos) atomicOr(&sbits[start >> 5], 1u << (start & 31));
         }
         if (n1 > 0) {
             const int st1 = start + n0;
             s_row[idx] = ((uint32_t)r << 25) | (uint32_t)(gb_[hh] - st1 + kRowBias);
-            if (FARMS_PAIR_BITCAP == 0 || st1 < FARMS_PAIR_BITCAP) atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
+            if (st1 < kPairBitPos) atomicOr(&sbits[st1 >> 5], 1u << (st1 & 31));
         }
         nz += (int)__popcll(b0) + (int)__popcll(b1);
         const int tA = __builtin_amdgcn_readlane(incl, 31), tB = __builtin_amdgcn_readlane(incl, 63);
@@ -3511,9 +3493,6 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     double pv0 = 0.0, pv1 = 0.0, pv2 = 0.0;
     int pk0 = K;
     int stA = 0, stB = 0;  // (wave-uniform) staged entries not yet folded, per event
-#if FARMS_PAIR_RING
-    int rdA = 0, rdB = 0;  // (wave-uniform) ring slot of the first of them (a multiple of 8)
-#endif
     for (int f0 = 0;; f0 += 32) {
         const bool have = f0 < tmax;  // wave-uniform
         bool con = false;
@@ -3562,11 +3541,7 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if ((pbal >> lane) & 1) {
-#if FARMS_PAIR_RING
-                const int slot = mbcnt64(pbal & hm, lane < 32 ? rdA + stA : rdB + stB) & (kPairSlots - 1);
-#else
                 const int slot = mbcnt64(pbal & hm, lane < 32 ? stA : stB);
-#endif
                 s_val[3 * slot] = pv0; s_val[3 * slot + 1] = pv1; s_val[3 * slot + 2] = pv2;
                 s_k0[slot] = (uint8_t)(pk0 > 0 ? 3 * (pk0 - 1) : 0);
                 atomicAdd(&s_hist[pk0], 1);
@@ -3580,28 +3555,18 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
             const int wA = stA & ~7, wB = stB & ~7;
             const int wmaxg = wA > wB ? wA : wB;
             const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
-#if FARMS_PAIR_RING
-            const int rd_h = lane < 32 ? rdA : rdB;
-#else
-            constexpr int rd_h = 0;
-#endif
 #pragma unroll 1
             for (int r = 0; r < wmaxg; r += 8) {
-                const int g = (rd_h + r) & (FARMS_PAIR_RING ? kPairSlots - 1 : 0x7FFFFFFF);
-                const uint32_t kw0 = k4p[g >> 2], kw1 = k4p[(g >> 2) + 1];
+                const uint32_t kw0 = k4p[r >> 2], kw1 = k4p[(r >> 2) + 1];
                 double vv[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (g + u) + q];
+                for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (r + u) + q];
                 const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
                 const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
                 fold8_pair(acc, r < wA ? a0 : kPairJunk, r < wA ? a1 : kPairJunk, r < wB ? b0 : kPairJunk,
                            r < wB ? b1 : kPairJunk, vv);
             }
             const int rA = stA - wA, rB = stB - wB;
-#if FARMS_PAIR_RING
-            rdA = (rdA + wA) & (kPairSlots - 1);
-            rdB = (rdB + wB) & (kPairSlots - 1);
-#else
             // carry each event's rest (< 8) to its slots [0, rest)
             const int w_h = lane < 32 ? wA : wB, r_h = lane < 32 ? rA : rB;
             if ((wA > 0 && rA > 0) || (wB > 0 && rB > 0)) {
@@ -3619,7 +3584,6 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
                     s_k0[hl] = mk;
                 }
             }
-#endif
             stA = rA;
             stB = rB;
         }
@@ -3633,19 +3597,14 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const int st_h = lane < 32 ? stA : stB;
-#if FARMS_PAIR_RING
-        const int g = lane < 32 ? rdA : rdB;
-#else
-        constexpr int g = 0;
-#endif
-        if (hl >= st_h && hl < 8) s_k0[g + hl] = (uint8_t)30;
+        if (hl >= st_h && hl < 8) s_k0[hl] = (uint8_t)30;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint32_t *k4p = reinterpret_cast<const uint32_t *>(s_k0);
-        const uint32_t kw0 = k4p[g >> 2], kw1 = k4p[(g >> 2) + 1];
+        const uint32_t kw0 = k4p[0], kw1 = k4p[1];
         double vv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * (g + u) + q];
+        for (int u = 0; u < 8; ++u) vv[u] = s_val[3 * u + q];
         const uint32_t a0 = __builtin_amdgcn_readlane(kw0, 0), a1 = __builtin_amdgcn_readlane(kw1, 0);
         const uint32_t b0 = __builtin_amdgcn_readlane(kw0, 32), b1 = __builtin_amdgcn_readlane(kw1, 32);
         fold8_pair(acc, stA > 0 ? a0 : kPairJunk, stA > 0 ? a1 : kPairJunk, stB > 0 ? b0 : kPairJunk,
@@ -3697,7 +3656,8 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
 // chunk ch takes its compacted events 2p and 2p + 1 (k_pool_compact); pairs
 // past the chunk's count leave at once.  Same occupancy cap as k_pool.
 template <int K, bool W7>
-__global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch1, const int32_t *nv) {
+__global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch1, const int32_t *nv, int4 *ovf,
+                                                           int *ovfn) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
     else asm volatile("" ::: FARMS_POOL_FLOOR_6);
@@ -3713,7 +3673,7 @@ __global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch
     const int cnt = nv[ch];
     if (2 * p >= cnt) return;
     const bool hasB = 2 * p + 1 < cnt;
-    const bool act = lane < 32 || hasB;
+    bool act = lane < 32 || hasB;
     // a half without an event takes event A's fields: lane 0's, by readlane.
     // (readfirstlane would read the first lane of the exec mask the compiler
     // evaluates this select under -- lane 32 when only the idle half is
@@ -3741,10 +3701,44 @@ __global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     int nseg;
     int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
-    if (FARMS_PAIR_BITCAP > 0 && total > FARMS_PAIR_BITCAP - 64) total = 0;  // (experiment: skipped)
+    if (act && total > kPairBitPos) {  // past the bitmap: to the overflow list, pooled by k_pool_ovf
+        if ((lane & 31) == 0) ovf[atomicAdd(ovfn, 1)] = d;
+        act = false;
+        total = 0;
+        nseg = 0;
+    }
     const int totA = __builtin_amdgcn_readlane(total, 0), totB = __builtin_amdgcn_readlane(total, 32);
     pool_pair<K>(c, lane, act, e, ex, ey, teu, buf, i_lo, total, totA, totB, s_start, s_row, s_val, s_k0, s_hist,
                  s_own, nseg);
+}
+
+// The events of one k_pool2 launch whose windows held more than kPairBitPos
+// candidates (ovf[0, *ovfn), their descriptors), one event per wave as k_pool
+// with the full bitmap, on the pooling stream right after the launch.  A fixed
+// grid that strides over the list: it leaves at once when the list is empty.
+constexpr int kPoolOvfBlocks = 64;
+template <int K, bool W7>
+__global__ __launch_bounds__(64) void k_pool_ovf(Ctx c, const int4 *ovf, const int *ovfn) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
+    if constexpr (W7) asm volatile("" ::: FARMS_POOL_FLOOR_7);
+    else asm volatile("" ::: FARMS_POOL_FLOOR_6);
+    const int cnt = *ovfn;
+    const int lane = threadIdx.x & 63;
+    uint64_t *s_start = s_dyn;
+    uint32_t *s_row = reinterpret_cast<uint32_t *>(s_start + c.pool_bw);
+    double *s_val = reinterpret_cast<double *>(s_start + c.pool_bw + c.pool_rs);
+    uint8_t *s_k0 = reinterpret_cast<uint8_t *>(s_val + 4 * kPoolSlots);
+    for (int i = (int)blockIdx.x; i < cnt; i += (int)gridDim.x) {
+        const int4 d = ovf[i];
+        const int e = d.x, ch = e / c.C2;
+        const int buf = (c.ring0 + ch) % c.NB;
+#ifdef FARMS_POOL_STAMPS
+        PoolSt pool_st = {};
+#endif
+        pool_event<K>(c, e, d.y, d.z, (uint32_t)d.w, buf, lane, ch * c.C2, s_start, s_row, s_val, s_k0 POOL_ST_ARG);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // Global flow vector -> record (vFlow.cpp:365-366) for every pooled (valid,
@@ -3920,6 +3914,8 @@ struct Work {
     int32_t *cbk = nullptr;                    // k_cand plan: first chunk reaching each chunk's kill window
     int32_t *bstart = nullptr;                 // k_cand: per chunk, the work-order start of each column band
     int32_t *nv = nullptr;                     // paired pooling: per chunk, its pooled events (k_pool_compact)
+    int4 *ovf = nullptr;                       // paired pooling: events past the pair bitmap (k_pool_ovf)
+    int *ovfn = nullptr;                       // ... their number per super-chunk (list at the super-chunk's first event)
     int4 *s2x = nullptr;                       // k_cand_export: per chunk, its S2 sources
     int32_t *s2b = nullptr;                    // ... and their column bands' starts
     void *cub_tmp = nullptr;
@@ -4044,7 +4040,7 @@ void free_workspace(Work &w) {
     dfree(w.iota); dfree(w.P); dfree(w.PT); dfree(w.link);
     dfree(w.Q); dfree(w.qe); dfree(w.fdesc); dfree(w.plane); dfree(w.wkey); dfree(w.wkey_sorted);
     dfree(w.valid); dfree(w.evf); dfree(w.dbg_tc); dfree(w.ctmin); dfree(w.ctmax);
-    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart); dfree(w.nv); dfree(w.s2x); dfree(w.s2b);
+    dfree(w.cpmax); dfree(w.cbk); dfree(w.bstart); dfree(w.nv); dfree(w.s2x); dfree(w.s2b); dfree(w.ovf); dfree(w.ovfn);
     dfree(w.cub_tmp);
     w.cub_bytes = 0;
     w.cap = 0;
@@ -4078,6 +4074,7 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         (rc = dalloc(&w.valid, cap)) || (rc = dalloc(&w.evf, cap)) || (rc = dalloc(&w.dbg_tc, cap)) ||
         (rc = dalloc(&w.ctmin, nch)) || (rc = dalloc(&w.ctmax, nch)) || (rc = dalloc(&w.cpmax, nch)) ||
         (rc = dalloc(&w.cbk, nch)) || (rc = dalloc(&w.bstart, nch * (h->nbands + 1))) || (rc = dalloc(&w.nv, nch)) ||
+        (rc = dalloc(&w.ovf, cap)) || (rc = dalloc(&w.ovfn, nch)) ||
         (rc = dalloc(&w.s2x, cap)) || (rc = dalloc(&w.s2b, nch * (h->nbands + 1)))) {
         free_workspace(w);
         return rc;
@@ -4255,11 +4252,14 @@ pool_launcher pool_for(int K, int fr) {
 }
 // Paired pooling (k_pool2, 2 <= K <= 11): grid = pair slots of chunks [ch0, ch1).
 template <int K, bool W7>
-void launch_pool2(const Ctx &c, int ch0, int ch1, const int32_t *nv, hipStream_t s) {
+void launch_pool2(const Ctx &c, int ch0, int ch1, const int32_t *nv, int4 *ovf, int *ovfn, hipStream_t s) {
     const size_t lds = sizeof(uint64_t) * 2 * (size_t)pair_half_words(pair_bw(c.pool_bw), c.pool_rs);
-    hipLaunchKernelGGL((k_pool2<K, W7>), dim3((ch1 - ch0) * (c.C2 >> 1)), dim3(64), lds, s, c, ch0, ch1, nv);
+    hipLaunchKernelGGL((k_pool2<K, W7>), dim3((ch1 - ch0) * (c.C2 >> 1)), dim3(64), lds, s, c, ch0, ch1, nv, ovf,
+                       ovfn);
+    const size_t lds1 = sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
+    hipLaunchKernelGGL((k_pool_ovf<K, W7>), dim3(kPoolOvfBlocks), dim3(64), lds1, s, c, ovf, ovfn);
 }
-typedef void (*pair_launcher)(const Ctx &, int, int, const int32_t *, hipStream_t);
+typedef void (*pair_launcher)(const Ctx &, int, int, const int32_t *, int4 *, int *, hipStream_t);
 template <bool W7>
 pair_launcher pair_for_cap(int K) {
     switch (K) {
@@ -4758,7 +4758,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             hipLaunchKernelGGL(k_flow, dim3(ceil_div(q1 - q0, 64)), dim3(64), 0, sc, c, q0, q1);
         }
         if (use_cand < 0) { int rc = decide_cand(); if (rc) return rc; }
-        if (use_cand) hipLaunchKernelGGL(k_cand_export, dim3(ch1 - ch0), dim3(256), 0, sc, c, ch0, ch1);
+        if (use_cand) hipLaunchKernelGGL(k_cand_export, dim3((ch1 - ch0) * h->nbands), dim3(64), 0, sc, c, ch0, ch1);
         for (int a = ch0; a < ch1; a += 64) {  // <= 64 chunks per launch (k_chain: their spans in one VGPR)
             const int b = std::min(a + 64, ch1);
             if (use_cand)
@@ -4768,7 +4768,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
                 hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
         }
         if (pl2) {  // pooled events compacted per chunk, for the pairs
-            hipLaunchKernelGGL(k_pool_compact, dim3(ch1 - ch0), dim3(256), 0, sc, c, ch0, ch1, w.nv);
+            hipLaunchKernelGGL(k_pool_compact, dim3(ch1 - ch0), dim3(256), 0, sc, c, ch0, ch1, w.nv, w.ovfn + S);
         } else {
             const int q0 = ch0 * h->pool_chunk, q1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
             hipLaunchKernelGGL(k_pool_desc, dim3(ceil_div(q1 - q0, 256)), dim3(256), 0, sc, c, q0, q1);
@@ -4778,7 +4778,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (prof) { int rc = mark(h, sp, &k0); if (rc) return rc; }
-        if (pl2) pl2(c, ch0, ch1, w.nv, sp);
+        if (pl2) pl2(c, ch0, ch1, w.nv, w.ovf + (int64_t)ch0 * h->pool_chunk, w.ovfn + S, sp);
         else pl(c, p0, p1, sp);
         if (prof) {
             int rc = mark(h, sp, &k1);
@@ -4973,6 +4973,8 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     // 113 instead of 97 ms at C3).
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (const char *v = getenv("FARMS_STREAM_PRIO"))  // =flat: every stream at the low end (A/B aid)
+        if (v[0] == 'f') prio_hi = prio_lo;
     if (hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&h->s_pool, hipStreamNonBlocking, prio_lo) != hipSuccess ||

@@ -646,6 +646,27 @@ def test_fit_streams_on_device_paths_are_bitwise_identical(fs, monkeypatch):
             assert bitwise_equal(ref, g), (streams, two_phase, compare(ref, g))
 
 
+def test_paired_pooling_overflow_past_the_pair_bitmap_is_bitwise(monkeypatch):
+    """An event whose window holds more than kPairBitPos (1,024) candidates
+    leaves the pair's bitmap: k_pool2 lists it and k_pool_ovf pools it one
+    event per wave with the full bitmap, right after the launch.  A C2 stream
+    with its stamps compressed 16x (dense windows) through both pooling kernels
+    gives the same bits, and the scan-width tail shows the path ran."""
+    ev = farms.synth_config(2, 200_001)
+    x, y, t, p = ev.relative()
+    t = (t // 16).astype(t.dtype)
+    outs, tail = {}, {}
+    for pairs in ("1", "0"):
+        monkeypatch.setenv("FARMS_POOL_PAIRS", pairs)
+        with farms.FlowManager(320, 320, 5, 5) as fm:
+            fm.set_profiling(True)
+            outs[pairs] = fm.process(x, y, t, p)
+            tail[pairs] = fm.stats()["pool_scan_max"]
+    assert tail["1"] > 1024, tail
+    assert bitwise_equal(outs["1"], outs["0"]), compare(outs["0"], outs["1"])
+    assert int((outs["1"].r_true != 0).sum()) > 1000
+
+
 @pytest.mark.parametrize("jump,maxw,pc", [(50, 50, 0), (25, 50, 0), (10, 50, 2048), (5, 50, 0), (4, 50, 0), (5, 20, 1024)])
 def test_paired_pooling_is_bitwise_one_event_per_wave(jump, maxw, pc, monkeypatch):
     """k_pool2 pools two events per wave (K <= 11 scales: 3 (K - 1) lanes per

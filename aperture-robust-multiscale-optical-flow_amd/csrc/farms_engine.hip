@@ -265,7 +265,8 @@ struct Ctx {
     // band's bstart index)
     int4 *s2x;
     int32_t *s2b;
-    int nbands, bandc;     // column bands, columns per band (bandc * H: whole candidate groups)
+    int nbands, bandc;     // column bands, columns per band (bandc * H: whole candidate groups; a power of two)
+    int band_slots;        // the call's candidate buffers hold k_cand's band-contiguous slots (else k_chain's)
     int tilesH, tshift;    // work-order tiles per column, log2 of the tile edge
     // serial mode (vFlowManager::run, vFlow.cpp:465-826): an event is pooled
     // with its pixel's lastEventTime still holding link.w, the stamp before it
@@ -1949,6 +1950,25 @@ __device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)acc));
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
+// 16-lane row, then the row broadcasts of lanes 15 and 31.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = (int)__lane_id(), rl = lane & 15;
+    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    if (rl >= 1) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    if (rl >= 2) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    if (rl >= 4) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    if (rl >= 8) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15
+    if ((lane & 31) >= 16) v += t;
+    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xF, 0xF, false);  // row_bcast:31
+    if (lane >= 32) v += t;
+    return v;
+}
+
 constexpr int kGroupCells = 256;
 
 // The call's candidate-build plan (Ctx::cinfo, per workspace set):
@@ -2412,7 +2432,6 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
     const uint32_t qa = (uint32_t)bd * (uint32_t)c.bandc * (uint32_t)H;
     const uint32_t qb = (uint32_t)min((int64_t)qa + (int64_t)c.bandc * H, c.WH);
     const int nw = (int)((qb - qa + 63) >> 6);
-    const int g0 = (int)(qa / kGroupCells);
     for (int i = lane; i < nw; i += 64) s_bm[i] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2502,22 +2521,34 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // bitmap words with the group-local offset of their first candidate
+    // bitmap words with the slot of their first candidate: the band's
+    // candidates take slots [qa, qa + count) in cell order (band-contiguous, so
+    // that a pooling row inside the band is one slot range: Ctx::band_slots)
     const int buf = (c.ring0 + ch) % c.NB;
     BmWord *bw = c.bw_ring + (int64_t)buf * c.nwords;
     const int64_t wbase = (int64_t)qa >> 6;
-    auto word_off = [&](int i) {  // candidate index of word i's first candidate
-        uint32_t wo = (uint32_t)(g0 + (i >> 2)) * kGroupCells;
-        for (int u = i & ~3; u < i; ++u) wo += (uint32_t)__popcll(s_bm[u]);
-        return wo;
-    };
-    for (int i = lane; i < nw; i += 64) {
-        BmWord v;
-        v.bm = s_bm[i];
-        v.wo = word_off(i);
-        v.pad = 0;
-        bw[wbase + i] = v;
+    uint32_t *s_wo = reinterpret_cast<uint32_t *>(s_bm + nw);
+    {
+        uint32_t carry = qa;  // (wave-uniform)
+        for (int i0 = 0; i0 < nw; i0 += 64) {
+            const int i = i0 + lane;
+            const uint64_t m = i < nw ? s_bm[i] : 0ull;
+            const int v = (int)__popcll(m);
+            const int incl = wave_incl_scan(v);
+            const uint32_t wo = carry + (uint32_t)(incl - v);
+            if (i < nw) {
+                s_wo[i] = wo;
+                BmWord bv;
+                bv.bm = m;
+                bv.wo = wo;
+                bv.pad = 0;
+                bw[wbase + i] = bv;
+            }
+            carry += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+        }
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     // the records
     cnt = min(cnt, cap);
     CandHdr *hr = c.hdr_ring + (int64_t)buf * c.cstride;
@@ -2573,7 +2604,7 @@ __global__ __launch_bounds__(64) void k_cand(Ctx c, int ch0, int ch1) {
             v.run_hi = 0;
         }
         const int wi = (int)((q - qa) >> 6);
-        const uint32_t slot = word_off(wi) + (uint32_t)__popcll(s_bm[wi] & ((1ull << (q & 63)) - 1));
+        const uint32_t slot = s_wo[wi] + (uint32_t)__popcll(s_bm[wi] & ((1ull << (q & 63)) - 1));
         hr[slot] = hd;
         if (item >= cs) {
             vr[slot] = v;
@@ -2617,25 +2648,6 @@ __device__ __forceinline__ int run_search_bounds(const Ctx &c, int lo, int hi, i
 template <class T>
 __device__ __forceinline__ const T &at32(const T *base, uint32_t i) {
     return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T)));
-}
-
-// Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
-// 16-lane row, then the row broadcasts of lanes 15 and 31.
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = (int)__lane_id(), rl = lane & 15;
-    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    if (rl >= 1) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    if (rl >= 2) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    if (rl >= 4) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    if (rl >= 8) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15
-    if ((lane & 31) >= 16) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xF, 0xF, false);  // row_bcast:31
-    if (lane >= 32) v += t;
-    return v;
 }
 
 // Max over the 64 lanes (exact).
@@ -2767,6 +2779,9 @@ __device__ __forceinline__ void fold8_k(double &acc, int kk, uint32_t kw0, uint3
 // s_start (bit f set iff a non-empty row segment starts at flattened position
 // f), s_row (the non-empty segments in order: {row, candidate index - flattened
 // index}).  Returns the flattened length.  LDS private to the calling wave.
+// The slot layouts of a chunk's candidate buffer (pool_rows / pool_rows2 MODE).
+constexpr int kSlotsGroup = 0, kSlotsBand = 1, kSlotsBandFlat = 2;
+template <int MODE>  // (the slot layout: see pool_rows2)
 __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_lo, int nrows, int j_lo, int j_hi,
                                          uint64_t *s_start, uint32_t *s_row) {
     const int H = c.H;
@@ -2805,29 +2820,48 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         l1 -= OFF;
         if (l0 < 0) l0 = 0;               // outside the stored region: never visited
         if (l1 > WHl - 1) l1 = WHl - 1;
-        const int gb = l1 & ~(kGroupCells - 1);  // first cell of l1's group
         has_[hh] = r < nrows && l0 <= l1;
-        str_[hh] = has_[hh] && l0 < gb;          // the range crosses into l1's group
+        int gb;
+        if constexpr (MODE == kSlotsGroup) {
+            gb = l1 & ~(kGroupCells - 1);            // first cell of l1's group
+            str_[hh] = has_[hh] && l0 < gb;          // the range crosses into l1's group
+        } else if constexpr (MODE == kSlotsBand) {
+            gb = base + H - OFF;                     // the next x-row's first cell, a band start or not
+            str_[hh] = has_[hh] && l0 < gb && gb <= l1 && ((i_lo + r + 1 - c.X0) & (c.bandc - 1)) == 0;
+        } else {
+            gb = 0;
+            str_[hh] = false;
+        }
         lo_[hh] = l0; gb_[hh] = gb;
         hi0_[hh] = str_[hh] ? gb - 1 : l1;       // end of the first segment
         hi1_[hh] = l1;
-        const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
-                  wc = min(max(l1 >> 6, 0), wmax);
-        const BmWord A = at32(bwb, (uint32_t)wa), B = at32(bwb, (uint32_t)wb), C = at32(bwb, (uint32_t)wc);
+        const int wa = min(max(l0 >> 6, 0), wmax), wc = min(max(l1 >> 6, 0), wmax);
+        const BmWord A = at32(bwb, (uint32_t)wa), C = at32(bwb, (uint32_t)wc);
         bA[hh] = A.bm; oA[hh] = A.wo;
-        bB[hh] = B.bm; oB[hh] = B.wo;
         bC[hh] = C.bm; oC[hh] = C.wo;
+        if constexpr (MODE != kSlotsBandFlat) {
+            const int wb = min(max(hi0_[hh] >> 6, 0), wmax);
+            const BmWord B = at32(bwb, (uint32_t)wb);
+            bB[hh] = B.bm; oB[hh] = B.wo;
+        } else {
+            bB[hh] = 0; oB[hh] = 0;
+        }
     }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
         // candidate index of the first candidate >= L (lo) / one past the last <= L (hi)
         const int lo = (int)(oA[hh] + (uint32_t)__popcll(bA[hh] & ((1ull << (lo_[hh] & 63)) - 1)));
-        const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
         const int h1 = (int)(oC[hh] + (uint32_t)__popcll(bC[hh] & ((2ull << (hi1_[hh] & 63)) - 1)));
         a0[hh] = lo;
-        n0[hh] = has_[hh] ? h0 - lo : 0;
         a1[hh] = gb_[hh];
-        n1[hh] = str_[hh] ? h1 - gb_[hh] : 0;
+        if constexpr (MODE == kSlotsBandFlat) {
+            n0[hh] = has_[hh] ? h1 - lo : 0;
+            n1[hh] = 0;
+        } else {
+            const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
+            n0[hh] = has_[hh] ? h0 - lo : 0;
+            n1[hh] = str_[hh] ? h1 - gb_[hh] : 0;
+        }
     }
     int carry = 0, nz = 0;
 #pragma unroll
@@ -2837,7 +2871,7 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         const int cnt = n0[hh] + n1[hh];
         const int incl = wave_incl_scan(cnt);
         const int start = carry + incl - cnt;
-        const uint64_t b0 = __ballot(n0[hh] > 0), b1 = __ballot(n1[hh] > 0);
+        const uint64_t b0 = __ballot(n0[hh] > 0), b1 = MODE == kSlotsBandFlat ? 0ull : __ballot(n1[hh] > 0);
         int idx = mbcnt64(b1, mbcnt64(b0, nz));
         if (n0[hh] > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(a0[hh] - start + kRowBias);
@@ -3164,7 +3198,10 @@ __device__ __forceinline__ void pool_event(const Ctx &c, int e, int ex, int ey, 
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
     POOL_CLOCK(tr0);
-    const int total = pool_rows(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    int total;  // (the layout branch is wave-uniform: one event per wave)
+    if (!c.band_slots) total = pool_rows<kSlotsGroup>(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    else if (j_hi >= c.H) total = pool_rows<kSlotsBand>(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
+    else total = pool_rows<kSlotsBandFlat>(c, buf, lane, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row);
     POOL_CLOCK(tr1);
     POOL_STAMP_ADD(1, tr1 - tr0);
     pool_one<K>(c, e, ex, ey, teu, buf, lane, i_lo, total, ev0, s_start, s_row, s_val, s_k0 POOL_ST_ARG);
@@ -3325,7 +3362,13 @@ __device__ __forceinline__ double half_max(double v) {
 
 // pool_rows for two windows: half h builds its event's row table (rows hl,
 // hl + 32, hl + 64, hl + 96) into its own LDS arrays; returns the half's
-// flattened length (0 for an absent event).
+// flattened length (0 for an absent event).  MODE: the chunk buffer's slot
+// layout (kSlotsGroup: k_chain's, a row segment splits where it crosses into
+// the next 256-cell group; kSlotsBand: k_cand's band-contiguous slots, a
+// segment splits only where the W - 1 clip carries it across a band boundary;
+// kSlotsBandFlat: the same for windows that stay inside their x-rows, where
+// no segment splits).
+template <int MODE>
 __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool act, int i_lo, int nrows, int j_lo,
                                           int j_hi, uint64_t *s_start, uint32_t *s_row, int &nseg) {
     const int H = c.H;
@@ -3359,32 +3402,53 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         l1 -= OFF;
         if (l0 < 0) l0 = 0;               // outside the stored region: never visited
         if (l1 > WHl - 1) l1 = WHl - 1;
-        const int gb = l1 & ~(kGroupCells - 1);
         has_[hh] = act && r < nrows && l0 <= l1;
-        str_[hh] = has_[hh] && l0 < gb;
+        int gb;
+        if constexpr (MODE == kSlotsGroup) {
+            gb = l1 & ~(kGroupCells - 1);
+            str_[hh] = has_[hh] && l0 < gb;
+        } else if constexpr (MODE == kSlotsBand) {
+            gb = base + H - OFF;  // the next x-row's first cell: a band start when that row's band index is whole
+            str_[hh] = has_[hh] && l0 < gb && gb <= l1 && ((i_lo + r + 1 - c.X0) & (c.bandc - 1)) == 0;
+        } else {
+            gb = 0;
+            str_[hh] = false;
+        }
         lo_[hh] = l0; gb_[hh] = gb;
         hi0_[hh] = str_[hh] ? gb - 1 : l1;
         hi1_[hh] = l1;
-        const int wa = min(max(l0 >> 6, 0), wmax), wb = min(max(hi0_[hh] >> 6, 0), wmax),
-                  wc = min(max(l1 >> 6, 0), wmax);
-        const BmWord A = at32(bwb, (uint32_t)wa), B = at32(bwb, (uint32_t)wb), C = at32(bwb, (uint32_t)wc);
+        const int wa = min(max(l0 >> 6, 0), wmax), wc = min(max(l1 >> 6, 0), wmax);
+        const BmWord A = at32(bwb, (uint32_t)wa), C = at32(bwb, (uint32_t)wc);
         bA[hh] = A.bm; oA[hh] = A.wo;
-        bB[hh] = B.bm; oB[hh] = B.wo;
         bC[hh] = C.bm; oC[hh] = C.wo;
+        if constexpr (MODE != kSlotsBandFlat) {
+            const int wb = min(max(hi0_[hh] >> 6, 0), wmax);
+            const BmWord B = at32(bwb, (uint32_t)wb);
+            bB[hh] = B.bm; oB[hh] = B.wo;
+        } else {
+            bB[hh] = 0; oB[hh] = 0;
+        }
     }
     int carry = 0, nz = 0;
 #pragma unroll
     for (int hh = 0; hh < NB; ++hh) {
         const int r = hl + 32 * hh;
         const int lo = (int)(oA[hh] + (uint32_t)__popcll(bA[hh] & ((1ull << (lo_[hh] & 63)) - 1)));
-        const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
         const int h1 = (int)(oC[hh] + (uint32_t)__popcll(bC[hh] & ((2ull << (hi1_[hh] & 63)) - 1)));
-        const int n0 = has_[hh] ? h0 - lo : 0;
-        const int n1 = str_[hh] ? h1 - gb_[hh] : 0;
+        int n0, n1;
+        if constexpr (MODE == kSlotsBandFlat) {
+            n0 = has_[hh] ? h1 - lo : 0;
+            n1 = 0;
+        } else {
+            const int h0 = (int)(oB[hh] + (uint32_t)__popcll(bB[hh] & ((2ull << (hi0_[hh] & 63)) - 1)));
+            n0 = has_[hh] ? h0 - lo : 0;
+            n1 = str_[hh] ? h1 - gb_[hh] : 0;
+        }
         const int cnt = n0 + n1;
         const int incl = half_incl_scan(cnt);
         const int start = carry + incl - cnt;
-        const uint64_t b0 = __ballot(n0 > 0) & hm, b1 = __ballot(n1 > 0) & hm;
+        const uint64_t b0 = __ballot(n0 > 0) & hm;
+        const uint64_t b1 = MODE == kSlotsBandFlat ? 0ull : __ballot(n1 > 0) & hm;
         int idx = mbcnt64(b1, mbcnt64(b0, nz));
         if (n0 > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
@@ -3699,8 +3763,14 @@ __global__ __launch_bounds__(64, W7 ? 7 : 6) void k_pool2(Ctx c, int ch0, int ch
     const int W = c.W, M = c.M;
     const int i_lo = ex - M < 0 ? 0 : ex - M, i_hi = ex + M > W - 1 ? W - 1 : ex + M;
     const int j_lo = ey - M < 0 ? 0 : ey - M, j_hi = ey + M > W - 1 ? W - 1 : ey + M;
-    int nseg;
-    int total = pool_rows2(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
+    int nseg, total;
+    if (!c.band_slots) {
+        total = pool_rows2<kSlotsGroup>(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
+    } else if (__ballot(act && j_hi >= c.H)) {  // a window clipped at W - 1 past its x-row (W > H): wave-uniform
+        total = pool_rows2<kSlotsBand>(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
+    } else {
+        total = pool_rows2<kSlotsBandFlat>(c, buf, lane, act, i_lo, i_hi - i_lo + 1, j_lo, j_hi, s_start, s_row, nseg);
+    }
     if (act && total > kPairBitPos) {  // past the bitmap: to the overflow list, pooled by k_pool_ovf
         if ((lane & 31) == 0) ovf[atomicAdd(ovfn, 1)] = d;
         act = false;
@@ -4394,7 +4464,7 @@ Ctx make_ctx(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     c.evf = w.evf; c.valid = w.valid; c.ctmin = w.ctmin; c.ctmax = w.ctmax;
     c.pcur = w.pcur; c.pend = w.pend;
     c.cbk = w.cbk; c.slist = w.slist; c.cinfo = w.cinfo; c.cscr = h->cscr;
-    c.bstart = w.bstart; c.nbands = h->nbands; c.bandc = h->bandc;
+    c.bstart = w.bstart; c.nbands = h->nbands; c.bandc = h->bandc; c.band_slots = 0;
     c.s2x = w.s2x; c.s2b = w.s2b;
     c.tshift = h->tile_shift; c.tilesH = (h->H + (1 << h->tile_shift) - 1) >> h->tile_shift;
     c.serial = h->prm.serial != 0;
@@ -4710,6 +4780,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             use_cand = h->plan_pin[&w - h->ws] <= kCandMaxBack;
         }
         h->cand_last = use_cand;
+        c.band_slots = use_cand ? 1 : 0;  // (the pooling launches below take c by value)
         if (use_cand)  // the call-start snapshot list (after the previous call's k_cand_commit on C)
             hipLaunchKernelGGL(k_cand_list, dim3(ceil_div(h->WH, 256)), dim3(256), 0, sc, c, w.slist);
         return FARMS_OK;
@@ -4763,7 +4834,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             const int b = std::min(a + 64, ch1);
             if (use_cand)
                 hipLaunchKernelGGL(k_cand, dim3((b - a) * h->nbands), dim3(64),
-                               sizeof(uint64_t) * (size_t)ceil_div((int64_t)h->bandc * h->H, 64), sc, c, a, b);
+                               (sizeof(uint64_t) + sizeof(uint32_t)) * (size_t)ceil_div((int64_t)h->bandc * h->H, 64),
+                               sc, c, a, b);
             else
                 hipLaunchKernelGGL(k_chain, dim3(h->nblk), dim3(64), 0, sc, c, a, b);
         }

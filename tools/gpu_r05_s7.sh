@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-5 session 7: k_cand's band-contiguous candidate slots (pooling rows as
+# one slot range): GPU parity suite, then C3 / C4 A/B against the previous build.
+cd /root/repo && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  > gpurun_out/r05_pytest_s7.log 2>&1 || exit 1
+L=gpurun_out/r05_ab_s7.log
+: > $L
+timeout -k 10 600 python3 -u tools/lib_ab.py --config 3 --steps 5 --rounds 2 build/libfarms_hip_r05a.so build/libfarms_hip.so >> $L 2>&1 || exit 2
+timeout -k 10 600 python3 -u tools/lib_ab.py --config 4 --steps 4 --rounds 2 build/libfarms_hip_r05a.so build/libfarms_hip.so >> $L 2>&1 || exit 3
+exit 0

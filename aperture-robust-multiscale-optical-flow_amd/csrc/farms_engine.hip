@@ -1953,19 +1953,13 @@ __device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
 // Inclusive prefix sum over the 64 lanes with DPP: row shifts inside each
 // 16-lane row, then the row broadcasts of lanes 15 and 31.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = (int)__lane_id(), rl = lane & 15;
-    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    if (rl >= 1) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    if (rl >= 2) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    if (rl >= 4) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    if (rl >= 8) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15
-    if ((lane & 31) >= 16) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x143, 0xF, 0xF, false);  // row_bcast:31
-    if (lane >= 32) v += t;
+    // (as half_incl_scan, then row_bcast:31 into rows 2 and 3)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
 
@@ -2835,13 +2829,15 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         lo_[hh] = l0; gb_[hh] = gb;
         hi0_[hh] = str_[hh] ? gb - 1 : l1;       // end of the first segment
         hi1_[hh] = l1;
-        const int wa = min(max(l0 >> 6, 0), wmax), wc = min(max(l1 >> 6, 0), wmax);
-        const BmWord A = at32(bwb, (uint32_t)wa), C = at32(bwb, (uint32_t)wc);
+        // word indices clamped for the loads only (a row without cells keeps has_
+        // false): l0 >= 0 here, and a negative l1 wraps to wmax as unsigned
+        const uint32_t wa = min((uint32_t)l0 >> 6, (uint32_t)wmax), wc = min((uint32_t)l1 >> 6, (uint32_t)wmax);
+        const BmWord A = at32(bwb, wa), C = at32(bwb, wc);
         bA[hh] = A.bm; oA[hh] = A.wo;
         bC[hh] = C.bm; oC[hh] = C.wo;
         if constexpr (MODE != kSlotsBandFlat) {
-            const int wb = min(max(hi0_[hh] >> 6, 0), wmax);
-            const BmWord B = at32(bwb, (uint32_t)wb);
+            const uint32_t wb = min((uint32_t)hi0_[hh] >> 6, (uint32_t)wmax);
+            const BmWord B = at32(bwb, wb);
             bB[hh] = B.bm; oB[hh] = B.wo;
         } else {
             bB[hh] = 0; oB[hh] = 0;
@@ -2872,7 +2868,7 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
         const int incl = wave_incl_scan(cnt);
         const int start = carry + incl - cnt;
         const uint64_t b0 = __ballot(n0[hh] > 0), b1 = MODE == kSlotsBandFlat ? 0ull : __ballot(n1[hh] > 0);
-        int idx = mbcnt64(b1, mbcnt64(b0, nz));
+        int idx = MODE == kSlotsBandFlat ? mbcnt64(b0, nz) : mbcnt64(b1, mbcnt64(b0, nz));
         if (n0[hh] > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(a0[hh] - start + kRowBias);
             atomicOr(&sbits[start >> 5], 1u << (start & 31));
@@ -3336,17 +3332,14 @@ __global__ __launch_bounds__(256) void k_pool_compact(Ctx c, int ch0, int ch1, i
 // Inclusive prefix sum within each 32-lane half (wave_incl_scan without its
 // last, half-crossing step).
 __device__ __forceinline__ int half_incl_scan(int v) {
-    const int lane = (int)__lane_id(), rl = lane & 15;
-    int t = __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    if (rl >= 1) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    if (rl >= 2) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    if (rl >= 4) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    if (rl >= 8) v += t;
-    t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15 (rows 1, 3 from rows 0, 2)
-    if ((lane & 31) >= 16) v += t;
+    // DPP with bound_ctrl: a lane without a source in its row reads 0, so each
+    // row shift is one DPP-fused add.  Full exec mask expected.
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    const int t = __builtin_amdgcn_mov_dpp(v, 0x142, 0xF, 0xF, false);  // row_bcast:15 (rows 1, 3 from rows 0, 2)
+    if ((__lane_id() & 31) >= 16) v += t;
     return v;
 }
 
@@ -3417,13 +3410,15 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         lo_[hh] = l0; gb_[hh] = gb;
         hi0_[hh] = str_[hh] ? gb - 1 : l1;
         hi1_[hh] = l1;
-        const int wa = min(max(l0 >> 6, 0), wmax), wc = min(max(l1 >> 6, 0), wmax);
-        const BmWord A = at32(bwb, (uint32_t)wa), C = at32(bwb, (uint32_t)wc);
+        // word indices clamped for the loads only (a row without cells keeps has_
+        // false): l0 >= 0 here, and a negative l1 wraps to wmax as unsigned
+        const uint32_t wa = min((uint32_t)l0 >> 6, (uint32_t)wmax), wc = min((uint32_t)l1 >> 6, (uint32_t)wmax);
+        const BmWord A = at32(bwb, wa), C = at32(bwb, wc);
         bA[hh] = A.bm; oA[hh] = A.wo;
         bC[hh] = C.bm; oC[hh] = C.wo;
         if constexpr (MODE != kSlotsBandFlat) {
-            const int wb = min(max(hi0_[hh] >> 6, 0), wmax);
-            const BmWord B = at32(bwb, (uint32_t)wb);
+            const uint32_t wb = min((uint32_t)hi0_[hh] >> 6, (uint32_t)wmax);
+            const BmWord B = at32(bwb, wb);
             bB[hh] = B.bm; oB[hh] = B.wo;
         } else {
             bB[hh] = 0; oB[hh] = 0;
@@ -3449,7 +3444,7 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
         const int start = carry + incl - cnt;
         const uint64_t b0 = __ballot(n0 > 0) & hm;
         const uint64_t b1 = MODE == kSlotsBandFlat ? 0ull : __ballot(n1 > 0) & hm;
-        int idx = mbcnt64(b1, mbcnt64(b0, nz));
+        int idx = MODE == kSlotsBandFlat ? mbcnt64(b0, nz) : mbcnt64(b1, mbcnt64(b0, nz));
         if (n0 > 0) {
             s_row[idx++] = ((uint32_t)r << 25) | (uint32_t)(lo - start + kRowBias);
             if (start < kPairBitPos) atomicOr(&sbits[start >> 5], 1u << (start & 31));

@@ -3167,21 +3167,20 @@ __device__ __forceinline__ void pool_finish(const Ctx &c, int e, int lane, doubl
     const double maxv = wave_max(mean);
     const int mi = maxv > 0 ? __builtin_ctzll(__ballot(is_len && mean == maxv)) : 0;
     const double sx = __shfl(acc, at(1, mi), 64), sy = __shfl(acc, at(2, mi), 64), cnt_mi = __shfl(acc, at(3, mi), 64);
-    if (lane == 0) {
-        double gx, gy;
-        int sc;
+    // lane 0 takes Gx, lane 1 Gy: one division sequence for both
+    if (lane < 2) {
+        double g;
         if (maxv > 0) {
-            gx = sx / cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
-            gy = sy / cnt_mi;
-            sc = mi * J;
+            g = (lane == 0 ? sx : sy) / cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
         } else {  // vFlow.cpp:1085-1094
-            const FlowCell self = c.evf[e];
-            gx = self.Lc; gy = self.Ls; sc = 0;
+            const FlowCell &self = c.evf[e];
+            g = lane == 0 ? self.Lc : self.Ls;
         }
-        c.r_true[e] = gx;  // (RTrue, ThetaTrue) by k_true_polar, 64 events per wave
-        c.th_true[e] = gy;
-        c.scale[e] = sc;
-        if (c.dbg_tc) c.dbg_tc[e] = make_int2(scanned, ncon_total);
+        (lane == 0 ? c.r_true : c.th_true)[e] = g;  // (RTrue, ThetaTrue) by k_true_polar, 64 events per wave
+        if (lane == 0) {
+            c.scale[e] = maxv > 0 ? mi * J : 0;
+            if (c.dbg_tc) c.dbg_tc[e] = make_int2(scanned, ncon_total);
+        }
     }
 }
 
@@ -3693,21 +3692,20 @@ __device__ __forceinline__ void pool_pair(const Ctx &c, int lane, bool act, int 
     const int src = base + 3 * (mi > 0 ? mi - 1 : 0);
     const double sx_s = __shfl(acc, src + 1, 64), sy_s = __shfl(acc, src + 2, 64);
     const double sx = mi == 0 ? s_own[1] : sx_s, sy = mi == 0 ? s_own[2] : sy_s;
-    if (act && hl == 0) {
-        double gx, gy;
-        int sc;
+    // lane 0 of the half takes Gx, lane 1 Gy: one division sequence for both
+    if (act && hl < 2) {
+        double g;
         if (maxv > 0) {
-            gx = sx / (double)cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
-            gy = sy / (double)cnt_mi;
-            sc = mi * J;
+            g = (hl == 0 ? sx : sy) / (double)cnt_mi;  // vFlow.cpp:1028-1029, 1067-1075
         } else {  // vFlow.cpp:1085-1094
-            const FlowCell self = c.evf[e];
-            gx = self.Lc; gy = self.Ls; sc = 0;
+            const FlowCell &self = c.evf[e];
+            g = hl == 0 ? self.Lc : self.Ls;
         }
-        c.r_true[e] = gx;  // (RTrue, ThetaTrue) by k_true_polar
-        c.th_true[e] = gy;
-        c.scale[e] = sc;
-        if (c.dbg_tc) c.dbg_tc[e] = make_int2(total, ncon);
+        (hl == 0 ? c.r_true : c.th_true)[e] = g;  // (RTrue, ThetaTrue) by k_true_polar
+        if (hl == 0) {
+            c.scale[e] = maxv > 0 ? mi * J : 0;
+            if (c.dbg_tc) c.dbg_tc[e] = make_int2(total, ncon);
+        }
     }
 }
 

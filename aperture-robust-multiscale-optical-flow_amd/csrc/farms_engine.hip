@@ -4024,11 +4024,17 @@ struct farms_handle {
     int64_t chunk_base = 0, super_base = 0;  // pooling chunks / super-chunks enqueued since the last reset
     hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
     hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
+    hipEvent_t ex_ev = nullptr;              // farms_export_flows_async: its gather done (stream F)
+    int ex_set = -1;                         // ... the workspace set it read (-1: none pending)
     hipStream_t polar_stream = nullptr;      // where the last k_true_polar was enqueued, and for which
     int64_t polar_super = -1;                // super-chunk (record_pool_done checks them)
     hipStream_t s_chain = nullptr, s_pool = nullptr;  // candidate-building chain, pooling kernels
     uint32_t seq = 0;
-    Work ws[2];
+    // workspace sets: device and host calls use sets 0 and 1; the two-phase
+    // calls rotate over all three, so that the fit of sub-batch b + 2 does not
+    // wait for the pooling of b (which held the x-strip pipeline's fits and
+    // poolings to taking turns)
+    Work ws[3];
     // two-phase calls (farms_fit_device / farms_pool_device): the fits not yet
     // pooled, oldest first (at most two: the fit of sub-batch b+1 may be issued
     // before the pooling of b), each on its own workspace set
@@ -4041,7 +4047,7 @@ struct farms_handle {
     };
     Phase ph[2] = {};
     int ph_count = 0;
-    uint32_t ph_seq = 0;  // fits issued: the next one's workspace set is ph_seq % 2
+    uint32_t ph_seq = 0;  // fits issued: the next one's workspace set is ph_seq % 3
     int64_t first_q = -1;       // serial mode: the first line's cell and stamp (farms_serial_first)
     uint32_t first_t = 0;
     bool fresh = true;          // no event since create / reset (farms_serial_first's precondition)
@@ -4509,10 +4515,10 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     if (!validated) {
         // on the copy stream: not behind F's work.  In device calls that stream
         // also runs the odd fit chunks (fs 7), so the host waits for the
-        // previous call's odd fits here -- in the x-strip pipeline those are
-        // already done (the exchange's export synchronized F behind them):
-        // farms_fit_device returns in 1.1-1.3 ms of host time there
-        // (profiles/r05_strip_host_times.log)
+        // previous call's odd fits here: in the x-strip pipeline, where the fit
+        // of b + 2 is issued under the fit of b + 1, that is the host's one
+        // wait per sub-batch (profiles/r05_strips_async_c4.log; the fits of
+        // two-phase calls on stream F alone instead: 99.7 against 77.2 ms)
         hipStream_t sv = h->s_copy;
         int herr = 0;
         HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), sv));
@@ -5046,8 +5052,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         hipStreamCreateWithPriority(&h->s_copy, hipStreamNonBlocking, prio_hi) != hipSuccess)  // (device calls: odd fits)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {
-        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end,
-                                         };
+        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->ex_ev};
         for (Work &w : h->ws) {
             evs.push_back(&w.done);
             evs.push_back(&w.ready);
@@ -5069,7 +5074,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
             (rc = dalloc(&w.slist, h->WH)) || (rc = dalloc(&w.cinfo, kCiWords)))
             return bail(rc);
     if ((rc = dalloc(&h->cscr, (size_t)std::min(h->pool_batch, 64) * h->WH))) return bail(rc);
-    if (hipHostMalloc((void **)&h->plan_pin, 2 * sizeof(int)) != hipSuccess)
+    if (hipHostMalloc((void **)&h->plan_pin, 3 * sizeof(int)) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipHostMalloc"));
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
@@ -5097,6 +5102,7 @@ extern "C" int farms_destroy(farms_handle *h) {
     for (auto &ev : h->up_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (h->chain_end) (void)hipEventDestroy(h->chain_end);
+    if (h->ex_ev) (void)hipEventDestroy(h->ex_ev);
     dfree(h->bw_ring); dfree(h->cscr);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &b : h->brk) {
@@ -5289,7 +5295,7 @@ extern "C" int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32
     if (rc) return rc;
     if (h->ph_count >= 2) return fail(FARMS_EINVAL, "two fits are already waiting for farms_pool_device");
     HIPCHK(hipSetDevice(h->prm.device));
-    const int set = (int)(h->ph_seq & 1);
+    const int set = (int)(h->ph_seq % 3);
     Work &w = h->ws[set];
     if (n > 0) {
         if ((rc = ensure_capacity(h, w, n))) return rc;
@@ -5317,27 +5323,53 @@ extern "C" int farms_pool_device(farms_handle *h) {
     return rc;
 }
 
-extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
+// The exchange acts on the oldest fit not yet pooled (h->ph[0]): the fit
+// whose pooling comes next.  (With one fit pending that is also the most recent
+// one; the asynchronous order issues the fit of b + 2 before the exchange of
+// b + 1, two fits pending.)
+namespace {
+int exchange_args(farms_handle *h, const void *d_idx, int64_t count, const void *d_flows, const char *what) {
     if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
         return fail(FARMS_EINVAL, "bad argument");
-    if (h->ph_count == 0) return fail(FARMS_EINVAL, "farms_export_flows outside a fit / pool pair");
+    if (h->ph_count == 0) return fail(FARMS_EINVAL, std::string(what) + " outside a fit / pool pair");
     HIPCHK(hipSetDevice(h->prm.device));
-    const farms_handle::Phase &f = h->ph[h->ph_count - 1];
+    return FARMS_OK;
+}
+}  // namespace
+
+extern "C" int farms_export_flows_async(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
+    if (int rc = exchange_args(h, d_idx, count, d_flows, "farms_export_flows")) return rc;
+    const farms_handle::Phase &f = h->ph[0];
+    // on stream F behind the fit's k_flow: a fit issued after this call runs
+    // behind the gather, and farms_export_wait waits for the gather only
     if (count > 0)
         hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->ws[f.set].evf,
                            d_idx, (int)count, d_flows);
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipEventRecord(h->ex_ev, h->stream));
     HIPCHK(hipGetLastError());
-    h->ws[f.set].ready_host = true;  // F drained: the fits of this phase are done
+    h->ex_set = f.set;
     return FARMS_OK;
 }
 
-extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows) {
-    if (!h || (count > 0 && (!d_idx || !d_flows)) || count < 0 || count >= INT_MAX)
-        return fail(FARMS_EINVAL, "bad argument");
-    if (h->ph_count == 0) return fail(FARMS_EINVAL, "farms_import_flows outside a fit / pool pair");
+extern "C" int farms_export_wait(farms_handle *h) {
+    if (!h) return fail(FARMS_EINVAL, "null handle");
+    if (h->ex_set < 0) return FARMS_OK;
     HIPCHK(hipSetDevice(h->prm.device));
-    const farms_handle::Phase &f = h->ph[h->ph_count - 1];
+    HIPCHK(hipEventSynchronize(h->ex_ev));
+    h->ws[h->ex_set].ready_host = true;  // the fits of that set are done (the gather ran behind them on F)
+    h->ex_set = -1;
+    return FARMS_OK;
+}
+
+extern "C" int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows) {
+    int rc = farms_export_flows_async(h, d_idx, count, d_flows);
+    if (!rc) rc = farms_export_wait(h);
+    return rc;
+}
+
+extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows) {
+    if (int rc = exchange_args(h, d_idx, count, d_flows, "farms_import_flows")) return rc;
+    const farms_handle::Phase &f = h->ph[0];
     Work &w = h->ws[f.set];
     Ctx c{};
     c.t = f.t; c.evf = w.evf; c.valid = w.valid;
@@ -5348,6 +5380,25 @@ extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
     w.ready_host = true;
+    return FARMS_OK;
+}
+
+extern "C" int farms_import_flows_async(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows) {
+    if (int rc = exchange_args(h, d_idx, count, d_flows, "farms_import_flows")) return rc;
+    const farms_handle::Phase &f = h->ph[0];
+    Work &w = h->ws[f.set];
+    // on the chain stream, behind the fit (w.ready: its phase-1 end on F, or an
+    // earlier import's mark): the pooling of this fit runs on that stream after
+    // it, and stream F -- with a later fit already queued -- stays free
+    hipStream_t sc = h->s_chain;
+    HIPCHK(hipStreamWaitEvent(sc, w.ready, 0));
+    Ctx c{};
+    c.t = f.t; c.evf = w.evf; c.valid = w.valid;
+    if (count > 0)
+        hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, sc, c, d_idx, (int)count, d_flows);
+    HIPCHK(hipEventRecord(w.ready, sc));
+    HIPCHK(hipGetLastError());
+    w.ready_host = false;  // (the pooling's chain waits w.ready: on its own stream, already in order)
     return FARMS_OK;
 }
 

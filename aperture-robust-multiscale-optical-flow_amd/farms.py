@@ -119,7 +119,8 @@ HIP_SYMBOLS = (
     "farms_process_device", "farms_set_profiling", "farms_get_stats", "farms_num_scales",
     "farms_get_last_event_time", "farms_last_error", "farms_last_stamps", "farms_merge_stamps",
     "farms_seed_sae", "farms_serial_first", "farms_fit_device", "farms_pool_device", "farms_export_flows",
-    "farms_import_flows", "farms_host_alloc", "farms_host_free", "farms_kernel_info",
+    "farms_import_flows", "farms_export_flows_async", "farms_export_wait", "farms_import_flows_async",
+    "farms_host_alloc", "farms_host_free", "farms_kernel_info",
 )
 SYNTH_SYMBOLS = ("farms_synth_preset", "farms_synth_generate", "farms_synth_write_text",
                  "farms_synth_generate_select", "farms_synth_column_hist")
@@ -508,6 +509,25 @@ class FlowManager:
         _check(self._lib, self._lib.farms_import_flows(self._h, ctypes.c_void_p(idx.data_ptr()),
                                                        ctypes.c_int64(int(idx.shape[0])),
                                                        ctypes.c_void_p(flows.data_ptr())))
+
+    def export_flows_async(self, idx, flows) -> None:
+        """export_flows without the wait: the gather is queued behind the fit
+        (export_wait before reading `flows`), so that the next fit_device can be
+        issued before the exchange completes."""
+        _check(self._lib, self._lib.farms_export_flows_async(self._h, ctypes.c_void_p(idx.data_ptr()),
+                                                             ctypes.c_int64(int(idx.shape[0])),
+                                                             ctypes.c_void_p(flows.data_ptr())))
+
+    def export_wait(self) -> None:
+        """Wait for the last export_flows_async's gather."""
+        _check(self._lib, self._lib.farms_export_wait(self._h))
+
+    def import_flows_async(self, idx, flows) -> None:
+        """import_flows queued ahead of the fit's pooling; `flows` stays valid and
+        unchanged until that pool_device has completed."""
+        _check(self._lib, self._lib.farms_import_flows_async(self._h, ctypes.c_void_p(idx.data_ptr()),
+                                                             ctypes.c_int64(int(idx.shape[0])),
+                                                             ctypes.c_void_p(flows.data_ptr())))
 
     def pool_device(self) -> None:
         """Phase 2: the pooling sweep of the events of the last fit_device."""

@@ -145,8 +145,10 @@ class Stepper:
     x-strips with the flow exchange run the step as a pipeline of `nsub`
     sub-batches cut at the same stream indices on every rank (so the per-
     sub-batch exchange lists pair up): the fit of sub-batch b+1 and its
-    exchange run while the pooling of b does (farms_fit_device /
-    farms_pool_device pipeline); consecutive sub-batches are bitwise one call."""
+    exchange run while the pooling of b does, and the fit of b+2 is issued
+    before that exchange is waited for (farms_fit_device / farms_pool_device
+    pipeline, the asynchronous exchange calls); consecutive sub-batches are
+    bitwise one call."""
 
     def __init__(self, eng, sh: Share, dist, device, xdev, nsub: int = 8):
         import torch
@@ -208,6 +210,14 @@ class Stepper:
         if self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
 
+    def _sync_current(self):
+        """Wait for the work issued on torch's current stream of the device (the
+        collectives and copies), not for the engine's streams."""
+        import torch
+
+        if self.dev.type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
+
     def step(self) -> None:
         import torch
 
@@ -219,29 +229,39 @@ class Stepper:
                 eng.fit_device(self.dx[lo:hi], self.dy[lo:hi], self.dt[lo:hi], self.dp[lo:hi],
                                {c: v[lo:hi] for c, v in self.out.items()})
 
-            def exchange(b):
+            def exchange(b, fit_next=None):
+                # the gathers of sub-batch b queued behind its fit; the fit of
+                # b + 1 (fit_next) issued before they are waited for, so that
+                # stream F is never idle across the exchange; the scatters queued
+                # ahead of b's pooling (each sub-batch its own buffer slices)
                 _, _, parts = self.sub[b]
                 sx, rx = {}, {}
                 for q, (si, ri, ss, rs) in parts.items():
-                    eng.export_flows(si, self.send_buf[q][ss])
+                    eng.export_flows_async(si, self.send_buf[q][ss])
+                if fit_next is not None:
+                    fit_next()
+                eng.export_wait()
+                for q, (si, ri, ss, rs) in parts.items():
                     if self.send_x[q] is not self.send_buf[q]:
                         self.send_x[q][ss].copy_(self.send_buf[q][ss])
                     sx[q], rx[q] = self.send_x[q][ss], self.recv_x[q][rs]
                 strips.exchange(d, sh.lists, sx, rx)
-                self._sync()
                 for q, (si, ri, ss, rs) in parts.items():
                     if self.recv_x[q] is not self.recv_buf[q]:
                         self.recv_buf[q][rs].copy_(self.recv_x[q][rs])
-                    eng.import_flows(ri, self.recv_buf[q][rs])
+                self._sync_current()  # the received flows in place (the current stream only)
+                for q, (si, ri, ss, rs) in parts.items():
+                    eng.import_flows_async(ri, self.recv_buf[q][rs])
 
+            # fit(b + 1) under the pooling of b; fit(b + 2) issued inside the
+            # exchange of b + 1 (at most two fits pending: farms_hip.h)
+            nsub = len(self.sub)
             fit(0)
-            exchange(0)
-            for b in range(len(self.sub)):
-                if b + 1 < len(self.sub):
-                    fit(b + 1)  # under the pooling of b
+            exchange(0, (lambda: fit(1)) if nsub > 1 else None)
+            for b in range(nsub):
                 eng.pool_device()
-                if b + 1 < len(self.sub):
-                    exchange(b + 1)
+                if b + 1 < nsub:
+                    exchange(b + 1, (lambda b2=b + 2: fit(b2)) if b + 2 < nsub else None)
             return
         if sh.seg is not None:
             o = sh.seg.n_warm  # the segment's own events start after the warm-up

@@ -153,7 +153,7 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
  * import_halo is set) over n device events; farms_export_flows (synchronous)
  * / farms_import_flows move the flows {L, L cos theta, L sin theta} (3 doubles
  * per listed event, d_idx = indices into those n events) out of / into the
- * handle for its most recent fit; farms_pool_device runs the pooling sweep of
+ * handle for its oldest fit not yet pooled; farms_pool_device runs the pooling sweep of
  * the oldest fit not yet pooled into its records.  A stream may be fed in
  * sub-batches, and the fit (and exchange) of sub-batch b+1 may be issued before
  * the pooling of b (at most two fits pending): that pooling then runs
@@ -166,6 +166,18 @@ int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, co
 int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows);
 int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows);
 int farms_pool_device(farms_handle *h);
+
+/* The same exchange without host waits on the device's other work, so that the
+ * fit of sub-batch b+2 can be issued before the exchange of b+1 completes (the
+ * x-strip pipeline): farms_export_flows_async enqueues the gather
+ * behind the fit's work and returns; farms_export_wait returns once d_flows
+ * holds it (waiting for nothing issued after the gather); farms_import_flows_async
+ * enqueues the scatter ahead of that fit's pooling and returns at once -- d_flows
+ * must stay valid and unchanged until the farms_pool_device of that fit has
+ * completed.  All exchange calls act on the oldest fit not yet pooled. */
+int farms_export_flows_async(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows);
+int farms_export_wait(farms_handle *h);
+int farms_import_flows_async(farms_handle *h, const int32_t *d_idx, int64_t count, const double *d_flows);
 
 /* Profiling of the next calls: FARMS_PROF_TIMING records HIP events around the
  * phases and every k_fit / k_pool launch on the stream that runs it (times in

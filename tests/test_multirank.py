@@ -76,13 +76,20 @@ class OracleEngine:
         self.pending.append({"ev": ev, "out": out, "fit": fit, "L": np.where(own, fit["r_local"], 0.0),
                              "th": np.where(own, fit["theta_local"], 0.0), "valid": own & gate(fit["vx"], fit["vy"])})
 
+    # the exchange acts on the oldest fit not yet pooled (farms_hip.h)
     def export_flows(self, idx, buf):
-        f, i = self.pending[-1], idx.numpy()
+        f, i = self.pending[0], idx.numpy()
         buf.copy_(torch.from_numpy(np.stack([f["L"][i], f["th"][i], f["valid"][i].astype(np.float64)], axis=1)))
 
     def import_flows(self, idx, buf):
-        f, i, b = self.pending[-1], idx.numpy(), buf.numpy()
+        f, i, b = self.pending[0], idx.numpy(), buf.numpy()
         f["L"][i], f["th"][i], f["valid"][i] = b[:, 0], b[:, 1], b[:, 2] > 0
+
+    export_flows_async = export_flows
+    import_flows_async = import_flows
+
+    def export_wait(self):
+        pass
 
     def pool_device(self):
         f = self.pending.pop(0)

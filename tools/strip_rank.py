@@ -119,25 +119,27 @@ for r in ranks:
         fm.reset()
         log.clear()
         if sh.lists is not None:
-            # the order of multirank.Stepper.step: fit b+1, pool b, then the
-            # exchange of b+1 (its export waits for the fit; import)
+            # the order of multirank.Stepper.step: the exchange of b+1 (its gather
+            # queued behind the fit) with the fit of b+2 issued before the wait,
+            # then the scatter queued ahead of the pooling of b+1
             def fit(b):
                 lo, hi, _, _ = subs[b]
                 timed(f"fit{b}", fm.fit_device, dx[lo:hi], dy[lo:hi], dt[lo:hi], dp[lo:hi],
                       {c: v[lo:hi] for c, v in out.items()})
 
-            def exchange(b):
+            def exchange(b, nxt):
                 _, _, hi_idx, hf = subs[b]
-                timed(f"export{b}", fm.export_flows, hi_idx[:1], ex_buf)
-                timed(f"import{b}", fm.import_flows, hi_idx, hf)
+                timed(f"export{b}", fm.export_flows_async, hi_idx[:1], ex_buf)
+                if nxt < len(subs):
+                    fit(nxt)
+                timed(f"wait{b}", fm.export_wait)
+                timed(f"import{b}", fm.import_flows_async, hi_idx, hf)
             fit(0)
-            exchange(0)
+            exchange(0, 1)
             for b in range(len(subs)):
-                if b + 1 < len(subs):
-                    fit(b + 1)
                 timed(f"pool{b}", fm.pool_device)
                 if b + 1 < len(subs):
-                    exchange(b + 1)
+                    exchange(b + 1, b + 2)
             return
         if seg:
             fm.last_stamps(dx[o:], dy[o:], dt[o:], sh.n_head, mine[0], mine[1])

@@ -686,3 +686,65 @@ def test_paired_pooling_is_bitwise_one_event_per_wave(jump, maxw, pc, monkeypatc
         assert kern.startswith(want), (kern, K)
     assert bitwise_equal(outs["1"], outs["0"]), compare(outs["0"], outs["1"])
     assert int((outs["1"].r_true != 0).sum()) > 1000
+
+
+@pytest.mark.parametrize("fs", [5, 7])
+def test_async_exchange_order_is_bitwise(fs):
+    """The x-strip stepper's order (multirank.Stepper.step): the gather of
+    sub-batch b queued behind its fit, the fit of b+1 issued before the host
+    waits for it (two fits pending, three workspace sets in rotation), the
+    scatter queued on the chain stream ahead of b's pooling.  Records bitwise
+    farms_process; the exported flows bitwise those of one fit at a time with
+    the synchronous farms_export_flows (the exchange calls act on the oldest
+    fit not yet pooled)."""
+    ev = farms.synth_config(4 if fs == 7 else 3, 200_000)
+    x, y, t, p = ev.relative()
+    with farms.FlowManager(720, 1280, fs, 5) as fm:
+        ref = fm.process(x, y, t, p)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x, y, t.view(np.int32), p)]
+    n = len(x)
+    splits = [(0, 50_000), (50_000, 50_001), (50_001, 120_000), (120_000, 160_000), (160_000, n)]
+    none = torch.zeros(0, dtype=torch.int32, device=dev)
+
+    def run(async_order):
+        o = {c: torch.zeros(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+             for c in farms.COLUMNS[4:]}
+        idx = [torch.arange(0, b - a, 5, dtype=torch.int32, device=dev) for a, b in splits]
+        bufs = [torch.full((len(i), 3), -1.0, dtype=torch.float64, device=dev) for i in idx]
+        with farms.FlowManager(720, 1280, fs, 5, fit_chunk=8192) as fm:
+            def fit(b):
+                a, e = splits[b]
+                fm.fit_device(*[v[a:e] for v in d], {c: v[a:e] for c, v in o.items()})
+
+            if async_order:
+                def exchange(b, nxt):
+                    fm.export_flows_async(idx[b], bufs[b])
+                    if nxt < len(splits):
+                        fit(nxt)
+                    fm.export_wait()
+                    fm.import_flows_async(none, bufs[b])
+                fit(0)
+                exchange(0, 1)
+                for b in range(len(splits)):
+                    fm.pool_device()
+                    if b + 1 < len(splits):
+                        exchange(b + 1, b + 2)
+            else:
+                for b in range(len(splits)):
+                    fit(b)
+                    fm.export_flows(idx[b], bufs[b])
+                    fm.import_flows(none, bufs[b])
+                    fm.pool_device()
+            torch.cuda.synchronize()
+        g = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
+        g.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
+        return g, [b.cpu().numpy() for b in bufs]
+
+    g_async, f_async = run(True)
+    g_sync, f_sync = run(False)
+    assert bitwise_equal(ref, g_async), compare(ref, g_async)
+    assert bitwise_equal(ref, g_sync), compare(ref, g_sync)
+    for a, b in zip(f_async, f_sync):
+        assert a.tobytes() == b.tobytes()
+        assert (a[:, 0] >= 0).all()  # every slot written

@@ -142,11 +142,11 @@ for r in ranks:
                     exchange(b + 1, b + 2)
             return
         if seg:
-            fm.last_stamps(dx[o:], dy[o:], dt[o:], sh.n_head, mine[0], mine[1])
+            timed("last_stamps", fm.last_stamps, dx[o:], dy[o:], dt[o:], sh.n_head, mine[0], mine[1])
             if r > 0:
-                fm.merge_stamps(stack, sae)
-                fm.seed_sae(sae)
-        fm.process_device(dx, dy, dt, dp, out)
+                timed("merge", fm.merge_stamps, stack, sae)
+                timed("seed", fm.seed_sae, sae)
+        timed("process", fm.process_device, dx, dy, dt, dp, out)
     run()  # warmup
     best = 1e9
     for _ in range(a.reps):

@@ -3855,6 +3855,129 @@ __global__ void k_last_index(const int32_t *x, const int32_t *y, int e0, int e1,
     atomicMax(&last[(int64_t)ex * H + ey], e);
 }
 
+// The same without scattered atomics (round 5: 50M device-scope atomicMax'es,
+// one lane per address, took 2.0 ms): the events bucketed by pixel tile
+// (kLastTile pixels) in two passes over blocks of kLastBlock events -- counts
+// per tile in LDS, one reservation per (block, tile), slots by LDS cursors --
+// then one workgroup per tile keeps its pixels' last event in LDS (for the
+// head [0, n_head) and for all events) and writes both stamp surfaces.
+// (blocks of 131,072 events: each block's per-tile counts go to global memory as
+// one-lane atomics, ≈900 per block at 1280x720, which at 16,384 events per
+// block made the two passes 1.4 ms of the call)
+constexpr int kLastTile = 1024, kLastBlock = 131072, kLastMaxTiles = 4096;
+__device__ __forceinline__ int last_pix(const int32_t *x, const int32_t *y, int e, int W, int H) {
+    const int ex = x[e], ey = y[e];
+    return (ex < 0 || ex >= W || ey < 0 || ey >= H) ? -1 : ex * H + ey;  // (rejected by farms_process* anyway)
+}
+__global__ __launch_bounds__(1024) void k_last_bucket(const int32_t *x, const int32_t *y, int n, int W, int H,
+                                                      int ntiles, int *tcount, int *tcur, int2 *bucket, int place) {
+    // a wave reads 64 consecutive events (coalesced); the lanes of one run of
+    // equal tiles make one LDS atomic, by the run's first lane.  (Measured: one
+    // LDS atomic per distinct tile of the wave, 3.3 ms a pass -- a wave's
+    // events span tens of tiles; a run of events per thread, 9 ms -- its loads
+    // uncoalesced.  What is left is the bucket pass's scattered 8-B writes.)
+    __shared__ int s_cnt[kLastMaxTiles], s_base[kLastMaxTiles];
+    for (int i = threadIdx.x; i < ntiles; i += blockDim.x) s_cnt[i] = 0;
+    __syncthreads();
+    const int lane = (int)threadIdx.x & 63;
+    const int e0 = blockIdx.x * kLastBlock, e1 = min(e0 + kLastBlock, n);
+    // per 64 events (their pixels q, -1: none): tile, the run heads' mask,
+    // this lane's head and, on a head, its run's length
+    auto runs = [&](int q, int &tl, int &head, int &len) {
+        tl = q < 0 ? -1 : q / kLastTile;
+        const int prev = __shfl_up(tl, 1, 64);
+        const uint64_t heads = __ballot(tl >= 0 && (lane == 0 || prev != tl));
+        const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        head = upto ? 63 - __clzll(upto) : 0;
+        // a head's run ends at the next head or at the first lane without a tile
+        const uint64_t none = __ballot(tl < 0);
+        const uint64_t stop = lane == 63 ? 0ull : (heads | none) >> (lane + 1);
+        len = stop ? __builtin_ctzll(stop) + 1 : 64 - lane;
+    };
+    for (int b = e0; b < e1; b += 4 * (int)blockDim.x) {
+        int qq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // four wave-batches' loads in flight together
+            const int e = b + u * (int)blockDim.x + (int)threadIdx.x;
+            qq[u] = e < e1 ? last_pix(x, y, e, W, H) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            int tl, head, len;
+            runs(qq[u], tl, head, len);
+            if (tl >= 0 && head == lane) atomicAdd(&s_cnt[tl], len);
+        }
+    }
+    __syncthreads();
+    if (!place) {  // pass 1: counts per tile
+        for (int i = threadIdx.x; i < ntiles; i += blockDim.x)
+            if (s_cnt[i]) atomicAdd(&tcount[i], s_cnt[i]);
+        return;
+    }
+    // pass 2: this block's range of each tile's bucket, then each run's slots
+    for (int i = threadIdx.x; i < ntiles; i += blockDim.x) {
+        s_base[i] = s_cnt[i] ? atomicAdd(&tcur[i], s_cnt[i]) : 0;
+        s_cnt[i] = 0;
+    }
+    __syncthreads();
+    for (int b = e0; b < e1; b += 4 * (int)blockDim.x) {
+        int qq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = b + u * (int)blockDim.x + (int)threadIdx.x;
+            qq[u] = e < e1 ? last_pix(x, y, e, W, H) : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = b + u * (int)blockDim.x + (int)threadIdx.x;
+            int tl, head, len;
+            runs(qq[u], tl, head, len);
+            int base = 0;
+            if (tl >= 0 && head == lane) base = s_base[tl] + atomicAdd(&s_cnt[tl], len);
+            base = __shfl(base, head, 64);
+            if (tl >= 0) bucket[base + (lane - head)] = make_int2(e, qq[u] - tl * kLastTile);
+        }
+    }
+}
+
+// tile offsets: tcur = exclusive prefix of tcount (one block; ntiles <= kLastMaxTiles)
+__global__ __launch_bounds__(1024) void k_last_offsets(const int *tcount, int ntiles, int *toff, int *tcur) {
+    __shared__ int s_sum[1024];
+    const int per = (ntiles + 1023) / 1024, i0 = threadIdx.x * per;
+    int v = 0;
+    for (int i = i0; i < min(i0 + per, ntiles); ++i) v += tcount[i];
+    s_sum[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = 0;
+        for (int i = 0; i < 1024; ++i) { const int c = s_sum[i]; s_sum[i] = a; a += c; }
+    }
+    __syncthreads();
+    int a = s_sum[threadIdx.x];
+    for (int i = i0; i < min(i0 + per, ntiles); ++i) { toff[i] = a; tcur[i] = a; a += tcount[i]; }
+    if (threadIdx.x == 1023) toff[ntiles] = a;
+}
+__global__ __launch_bounds__(256) void k_last_tile(const int2 *bucket, const int *toff, int n_head, const uint32_t *t,
+                                                   int64_t WH, int64_t *head, int64_t *full) {
+    __shared__ int s_head[kLastTile], s_full[kLastTile];
+    for (int i = threadIdx.x; i < kLastTile; i += blockDim.x) { s_head[i] = -1; s_full[i] = -1; }
+    __syncthreads();
+    const int tl = blockIdx.x;
+    for (int i = toff[tl] + (int)threadIdx.x; i < toff[tl + 1]; i += blockDim.x) {
+        const int2 b = bucket[i];
+        atomicMax(&s_full[b.y], b.x);
+        if (b.x < n_head) atomicMax(&s_head[b.y], b.x);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kLastTile; i += blockDim.x) {
+        const int64_t q = (int64_t)tl * kLastTile + i;
+        if (q >= WH) break;
+        const int ef = s_full[i], eh = s_head[i];
+        full[q] = ef >= 0 ? (int64_t)t[ef] : int64_t(-1);
+        if (head) head[q] = eh >= 0 ? (int64_t)t[eh] : int64_t(-1);
+    }
+}
+
 __global__ void k_last_stamp(const int32_t *last, const uint32_t *t, int64_t WH, int64_t *out) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= WH) return;
@@ -4025,6 +4148,8 @@ struct farms_handle {
     hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
     hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
     hipEvent_t ex_ev = nullptr;              // farms_export_flows_async: its gather done (stream F)
+    void *last_buf = nullptr;                // farms_last_stamps: tile counts and event buckets (grown on demand)
+    size_t last_cap = 0;
     int ex_set = -1;                         // ... the workspace set it read (-1: none pending)
     hipStream_t polar_stream = nullptr;      // where the last k_true_polar was enqueued, and for which
     int64_t polar_super = -1;                // super-chunk (record_pool_done checks them)
@@ -5103,6 +5228,7 @@ extern "C" int farms_destroy(farms_handle *h) {
         if (ev) (void)hipEventDestroy(ev);
     if (h->chain_end) (void)hipEventDestroy(h->chain_end);
     if (h->ex_ev) (void)hipEventDestroy(h->ex_ev);
+    if (h->last_buf) (void)hipFree(h->last_buf);
     dfree(h->bw_ring); dfree(h->cscr);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);
     for (auto &b : h->brk) {
@@ -5219,6 +5345,36 @@ extern "C" int farms_last_stamps(farms_handle *h, const int32_t *d_x, const int3
     HIPCHK(hipSetDevice(h->prm.device));
     const int64_t WHs = (int64_t)h->W * h->H;
     hipStream_t s = h->stream;
+    const int64_t ntiles = ceil_div(WHs, (int64_t)kLastTile);
+    if (ntiles <= kLastMaxTiles) {  // bucketed (no scattered global atomics)
+        const int nt = (int)ntiles;
+        const size_t cnt_bytes = (sizeof(int) * (3 * (size_t)nt + 1) + 15) & ~(size_t)15;
+        const size_t need = cnt_bytes + sizeof(int2) * (size_t)n;
+        if (need > h->last_cap) {
+            HIPCHK(hipStreamSynchronize(s));
+            if (h->last_buf) HIPCHK(hipFree(h->last_buf));
+            h->last_buf = nullptr;
+            h->last_cap = 0;
+            HIPCHK(hipMalloc(&h->last_buf, need));
+            h->last_cap = need;
+        }
+        int *cnt = static_cast<int *>(h->last_buf);  // tcount, tcur, toff (+1), then the buckets
+        int2 *bucket = reinterpret_cast<int2 *>(static_cast<char *>(h->last_buf) + cnt_bytes);
+        int *tcount = cnt, *tcur = cnt + nt, *toff = cnt + 2 * nt;
+        HIPCHK(hipMemsetAsync(tcount, 0, sizeof(int) * nt, s));
+        const int nb = (int)ceil_div(n, (int64_t)kLastBlock);
+        if (nb > 0)
+            hipLaunchKernelGGL(k_last_bucket, dim3(nb), dim3(1024), 0, s, d_x, d_y, (int)n, h->W, h->H, nt, tcount, tcur,
+                               bucket, 0);
+        hipLaunchKernelGGL(k_last_offsets, dim3(1), dim3(1024), 0, s, tcount, nt, toff, tcur);
+        if (nb > 0)
+            hipLaunchKernelGGL(k_last_bucket, dim3(nb), dim3(1024), 0, s, d_x, d_y, (int)n, h->W, h->H, nt, tcount, tcur,
+                               bucket, 1);
+        hipLaunchKernelGGL(k_last_tile, dim3(nt), dim3(256), 0, s, bucket, toff, (int)n_head, d_t, WHs, d_head, d_full);
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipGetLastError());
+        return FARMS_OK;
+    }
     int32_t *last = nullptr;
     HIPCHK(hipMallocAsync((void **)&last, sizeof(int32_t) * WHs, s));
     HIPCHK(hipMemsetAsync(last, 0xFF, sizeof(int32_t) * WHs, s));  // -1: no event

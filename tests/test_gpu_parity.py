@@ -73,6 +73,7 @@ def test_configs_vs_oracle(cfg, n, fs):
     assert rep["valid_ref"] > n // 20  # the stream really exercises pooling
 
 
+@pytest.mark.timeout(600)  # three CPU oracle passes over 2M events: past 120 s on a busy host
 def test_config2_full_stream_vs_oracle():
     """BASELINE config 2 at its full size (2M events, 320 x 320, fs 5): every
     record against the oracle (both libms, run in parallel threads: ~40 s

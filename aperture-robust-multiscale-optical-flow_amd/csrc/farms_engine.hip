@@ -4466,12 +4466,14 @@ pair_launcher pair_for_cap(int K) {
 }
 // Pairs are the default beside the fs <= 5 fits: C3 75.4 -> 73.0 ms per step.
 // Beside the fs-7 fit (10.8 KB of LDS per wave, the sweep that paces C4/C5)
-// the pairs' 6.4 KB per wave cost fit waves: C4 54.5 -> 55.8 ms, so fs 7 keeps
-// one event per wave (profiles/r05_ab_pool_pairs.log).  FARMS_POOL_PAIRS=0|1
-// overrides (A/B and test aid; the same bits).  Pairs need even pooling chunks
-// (the pair slots of a chunk).
+// the pairs' 6.4 KB per wave first cost fit waves: C4 54.5 -> 55.8 ms
+// (profiles/r05_ab_pool_pairs.log).  With the 4.1-KB pair bitmap and the
+// band-contiguous slots they pay at 11 scales (C4 53.1 -> 52.8 ms) and still
+// not at 3 (C5 63.2 -> 66.2, profiles/r05_ab_pairs_fs7_final.log): at fs 7
+// pairs from 8 scales up.  FARMS_POOL_PAIRS=0|1 overrides (A/B and test aid;
+// the same bits).  Pairs need even pooling chunks (the pair slots of a chunk).
 pair_launcher pair_for(int K, int fr, int pool_chunk) {
-    bool on = fr <= 2;
+    bool on = fr <= 2 || K >= 8;
     if (const char *v = getenv("FARMS_POOL_PAIRS")) on = v[0] != '0';
     if (!on || (pool_chunk & 1)) return nullptr;
     return pool_w7(fr) ? pair_for_cap<true>(K) : pair_for_cap<false>(K);

@@ -1976,6 +1976,7 @@ enum { kCiMaxBack = 0, kCiCount, kCiLMin, kCiLMax, kCiTMin, kCiTMax, kCiWords };
 // keep k_chain, whose cost is independent of the order.  The host reads the
 // reach after the call's prep (k_cand_plan_back) and launches one of the two.
 constexpr int kCandMaxBack = 64;
+constexpr int kPoisonByte = 0x7F;  // FARMS_POISON's fill (farms_handle::poison)
 
 
 // The pooling sweep's candidate chain, one launch per super-chunk (pooling
@@ -2775,6 +2776,17 @@ __device__ __forceinline__ void fold8_k(double &acc, int kk, uint32_t kw0, uint3
 // index}).  Returns the flattened length.  LDS private to the calling wave.
 // The slot layouts of a chunk's candidate buffer (pool_rows / pool_rows2 MODE).
 constexpr int kSlotsGroup = 0, kSlotsBand = 1, kSlotsBandFlat = 2;
+// kSlotsBand: the local cell where the band after the one holding a window
+// row's first cell starts, for the row of absolute x-row i (its first cell is
+// in local x-row i - X0, or in local cell 0 when the row starts left of the
+// stored region).  A row range is at most 2M + 1 <= 127 cells and a band at
+// least 256 (bandc H, whole candidate groups), so a range splits at most once,
+// and there.  The W - 1 clip can carry a range over more than one x-row (H <=
+// M): the band start is then not always the next x-row's first cell.
+__device__ __forceinline__ int band_split(const Ctx &c, int i) {
+    const int cs = i - c.X0;
+    return (((cs < 0 ? 0 : cs) | (c.bandc - 1)) + 1) * c.H;
+}
 template <int MODE>  // (the slot layout: see pool_rows2)
 __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_lo, int nrows, int j_lo, int j_hi,
                                          uint64_t *s_start, uint32_t *s_row) {
@@ -2820,8 +2832,8 @@ __device__ __forceinline__ int pool_rows(const Ctx &c, int buf, int lane, int i_
             gb = l1 & ~(kGroupCells - 1);            // first cell of l1's group
             str_[hh] = has_[hh] && l0 < gb;          // the range crosses into l1's group
         } else if constexpr (MODE == kSlotsBand) {
-            gb = base + H - OFF;                     // the next x-row's first cell, a band start or not
-            str_[hh] = has_[hh] && l0 < gb && gb <= l1 && ((i_lo + r + 1 - c.X0) & (c.bandc - 1)) == 0;
+            gb = band_split(c, i_lo + r);            // the first band start past l0
+            str_[hh] = has_[hh] && gb <= l1;
         } else {
             gb = 0;
             str_[hh] = false;
@@ -3400,8 +3412,8 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
             gb = l1 & ~(kGroupCells - 1);
             str_[hh] = has_[hh] && l0 < gb;
         } else if constexpr (MODE == kSlotsBand) {
-            gb = base + H - OFF;  // the next x-row's first cell: a band start when that row's band index is whole
-            str_[hh] = has_[hh] && l0 < gb && gb <= l1 && ((i_lo + r + 1 - c.X0) & (c.bandc - 1)) == 0;
+            gb = band_split(c, i_lo + r);  // the first band start past l0
+            str_[hh] = has_[hh] && gb <= l1;
         } else {
             gb = 0;
             str_[hh] = false;
@@ -3821,19 +3833,24 @@ __global__ void k_true_polar(Ctx c, int e0, int e1) {
 // {L, L cos(theta), L sin(theta)} of listed events out of / into evf.  An
 // imported flow takes the local event's stamp; validity is L > 0 (the gate's
 // L = 0 for an invalid event, vFlow.cpp:398-402).
-__global__ void k_export_flows(const FlowCell *evf, const int32_t *idx, int count, double *out) {
+// An index outside the fit's events [0, n) is skipped (its slot / nothing is
+// written) and counted in *bad: the synchronous calls report it.
+__global__ void k_export_flows(const FlowCell *evf, const int32_t *idx, int count, int n, double *out, int *bad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    const FlowCell f = evf[idx[i]];
+    const int e = idx[i];
+    if (e < 0 || e >= n) { atomicAdd(bad, 1); return; }
+    const FlowCell f = evf[e];
     out[3 * (int64_t)i] = f.L;
     out[3 * (int64_t)i + 1] = f.Lc;
     out[3 * (int64_t)i + 2] = f.Ls;
 }
 
-__global__ void k_import_flows(Ctx c, const int32_t *idx, int count, const double *in) {
+__global__ void k_import_flows(Ctx c, const int32_t *idx, int count, const double *in, int *bad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const int e = idx[i];
+    if (e < 0 || e >= c.n) { atomicAdd(bad, 1); return; }
     FlowCell f;
     f.L = in[3 * (int64_t)i];
     f.Lc = in[3 * (int64_t)i + 1];
@@ -4178,11 +4195,20 @@ struct farms_handle {
     bool fresh = true;          // no event since create / reset (farms_serial_first's precondition)
     int tile_bits = 0;
     int tile_shift = 3;       // work-order tile: 2^tile_shift square
-    int *err = nullptr;
+    int *err = nullptr;       // device words: [0] range check, [1] k_prep, [2] export / [3] import index check, [4] async import
+    int *err_pin = nullptr;   // pinned host copies of those words
     unsigned long long *counters = nullptr;
     bool profiling = false;  // kernel timing events
     bool counting = false;   // work counters (k_stats, per-event candidate counts)
     bool fit_events = false;  // timing events around every fit launch too
+    // FARMS_POISON=1 (test aid): before every call the per-event workspace the
+    // call must write before it reads it -- descriptors, links, planes, flows,
+    // accepted flags, the overflow list -- and, before each super-chunk's
+    // candidate build, the ring buffers it is about to fill start out as 0x7F
+    // bytes (event ids and slot indices ~2^31: any read of a word the call has
+    // not written goes far out of range instead of finding an earlier call's
+    // data, which fresh allocations hide behind zeros)
+    bool poison = false;
     // Profiling across calls (farms_get_stats reports the calls since the last
     // reset): each call records timing brackets -- its phases and its kernel
     // launches -- on the streams that run them, synchronous or not; they are
@@ -4636,6 +4662,16 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     int rc = claim_set(h, w, n, t_prep ? &t_start : nullptr);
     if (rc) return rc;
     hipStream_t s = h->stream;
+    if (h->poison) {  // (test aid, farms_handle::poison) after the set's previous call
+        const size_t cap = (size_t)w.cap;
+        HIPCHK(hipMemsetAsync(w.qe, kPoisonByte, sizeof(int4) * cap, s));
+        HIPCHK(hipMemsetAsync(w.fdesc, kPoisonByte, sizeof(int4) * cap, s));
+        HIPCHK(hipMemsetAsync(w.link, kPoisonByte, sizeof(int4) * cap, s));
+        HIPCHK(hipMemsetAsync(w.plane, kPoisonByte, sizeof(double2) * cap, s));
+        HIPCHK(hipMemsetAsync(w.evf, kPoisonByte, sizeof(FlowCell) * cap, s));
+        HIPCHK(hipMemsetAsync(w.valid, kPoisonByte, sizeof(uint8_t) * cap, s));
+        HIPCHK(hipMemsetAsync(w.ovf, kPoisonByte, sizeof(int4) * cap, s));
+    }
     const int n_pool_chunks = ceil_div(n, h->pool_chunk);
     const uint32_t *dt = c.t;
     hipEvent_t ev_prep = w.sync_ev[0];
@@ -4946,6 +4982,14 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
         if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
+        if (h->poison) {  // (test aid) the buffers the candidate build is about to fill
+            for (int ch = ch0; ch < ch1; ++ch) {
+                const int64_t buf = (c.ring0 + ch) % h->NB;
+                HIPCHK(hipMemsetAsync(h->hdr_ring + buf * h->cstride, kPoisonByte, sizeof(CandHdr) * h->cstride, sc));
+                HIPCHK(hipMemsetAsync(h->val_ring + buf * h->cstride, kPoisonByte, sizeof(CandVal) * h->cstride, sc));
+                HIPCHK(hipMemsetAsync(h->bw_ring + buf * h->nwords, kPoisonByte, sizeof(BmWord) * h->nwords, sc));
+            }
+        }
         if (phase == 0) {  // the super-chunk's local flows from its planes (phase 2: done by phase 1)
             const int fl = std::min((int)(((int64_t)ch1 * h->pool_chunk - 1) / h->fit_chunk), n_fit_chunks - 1);
             HIPCHK(hipStreamWaitEvent(sc, ev_fit(fl), 0));
@@ -5149,6 +5193,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
     {
         // FARMS_TILE_SHIFT (2..5, A/B aid): log2 of the work-order tile's edge
         if (const char *ts = getenv("FARMS_TILE_SHIFT")) h->tile_shift = std::max(2, std::min(atoi(ts), 5));
+        if (const char *pz = getenv("FARMS_POISON")) h->poison = pz[0] == '1';
         const int tm = (1 << h->tile_shift) - 1;
         const int64_t tiles = (int64_t)((h->W + tm) >> h->tile_shift) * ((h->H + tm) >> h->tile_shift);
         while ((int64_t(1) << h->tile_bits) < tiles) ++h->tile_bits;
@@ -5194,15 +5239,17 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         (rc = dalloc(&h->ftime, h->WH)) ||
         (rc = dalloc(&h->fsnap, h->WH)) ||
         (rc = dalloc(&h->bw_ring, h->nwords * h->NB)) || (rc = dalloc(&h->hdr_ring, h->cstride * h->NB)) ||
-        (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 2)) || (rc = dalloc(&h->counters, 8)))
+        (rc = dalloc(&h->val_ring, h->cstride * h->NB)) || (rc = dalloc(&h->err, 8)) || (rc = dalloc(&h->counters, 8)))
         return bail(rc);
     for (Work &w : h->ws)
         if ((rc = dalloc(&w.pcur, h->WH)) || (rc = dalloc(&w.pend, h->WH)) ||
             (rc = dalloc(&w.slist, h->WH)) || (rc = dalloc(&w.cinfo, kCiWords)))
             return bail(rc);
     if ((rc = dalloc(&h->cscr, (size_t)std::min(h->pool_batch, 64) * h->WH))) return bail(rc);
-    if (hipHostMalloc((void **)&h->plan_pin, 3 * sizeof(int)) != hipSuccess)
+    if (hipHostMalloc((void **)&h->plan_pin, (3 + 8) * sizeof(int)) != hipSuccess)
         return bail(fail(FARMS_EHIP, "hipHostMalloc"));
+    h->err_pin = h->plan_pin + 3;  // (one pinned block: freed with plan_pin)
+    std::fill(h->err_pin, h->err_pin + 8, 0);
     if ((rc = reset_surfaces(h))) return bail(rc);
     *out = h;
     return FARMS_OK;
@@ -5444,7 +5491,9 @@ int check_device_call(farms_handle *h, const int32_t *d_x, const int32_t *d_y, c
 
 // Two-phase calls pipeline: farms_fit_device enqueues its sub-batch's prep and
 // fits on the next workspace set and returns; the exports / imports act on the
-// most recent fit; farms_pool_device enqueues the pooling of the oldest fit not
+// oldest fit not yet pooled (h->ph[0], whose pooling comes next: with two fits
+// pending that is not the most recent one); farms_pool_device enqueues the
+// pooling of the oldest fit not
 // yet pooled -- asynchronously when a later fit is pending (its fits and the
 // halo exchange then run under this pooling), else it waits for the device.
 extern "C" int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t,
@@ -5500,9 +5549,14 @@ extern "C" int farms_export_flows_async(farms_handle *h, const int32_t *d_idx, i
     const farms_handle::Phase &f = h->ph[0];
     // on stream F behind the fit's k_flow: a fit issued after this call runs
     // behind the gather, and farms_export_wait waits for the gather only
-    if (count > 0)
+    if (count > 0) {
+        HIPCHK(hipMemsetAsync(h->err + 2, 0, sizeof(int), h->stream));
         hipLaunchKernelGGL(k_export_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, h->ws[f.set].evf,
-                           d_idx, (int)count, d_flows);
+                           d_idx, (int)count, (int)f.n, d_flows, h->err + 2);
+        HIPCHK(hipMemcpyAsync(h->err_pin + 2, h->err + 2, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    } else {
+        h->err_pin[2] = 0;
+    }
     HIPCHK(hipEventRecord(h->ex_ev, h->stream));
     HIPCHK(hipGetLastError());
     h->ex_set = f.set;
@@ -5516,6 +5570,7 @@ extern "C" int farms_export_wait(farms_handle *h) {
     HIPCHK(hipEventSynchronize(h->ex_ev));
     h->ws[h->ex_set].ready_host = true;  // the fits of that set are done (the gather ran behind them on F)
     h->ex_set = -1;
+    if (h->err_pin[2]) return fail(FARMS_EINVAL, "farms_export_flows: an index outside the fit's events (slot not written)");
     return FARMS_OK;
 }
 
@@ -5530,14 +5585,19 @@ extern "C" int farms_import_flows(farms_handle *h, const int32_t *d_idx, int64_t
     const farms_handle::Phase &f = h->ph[0];
     Work &w = h->ws[f.set];
     Ctx c{};
-    c.t = f.t; c.evf = w.evf; c.valid = w.valid;
-    if (count > 0)
+    c.t = f.t; c.evf = w.evf; c.valid = w.valid; c.n = (int)f.n;
+    h->err_pin[3] = 0;
+    if (count > 0) {
+        HIPCHK(hipMemsetAsync(h->err + 3, 0, sizeof(int), h->stream));
         hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, h->stream, c, d_idx, (int)count,
-                           d_flows);
+                           d_flows, h->err + 3);
+        HIPCHK(hipMemcpyAsync(h->err_pin + 3, h->err + 3, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    }
     HIPCHK(hipEventRecord(w.ready, h->stream));  // the pooling of this fit waits for its imports
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipGetLastError());
     w.ready_host = true;
+    if (h->err_pin[3]) return fail(FARMS_EINVAL, "farms_import_flows: an index outside the fit's events (skipped)");
     return FARMS_OK;
 }
 
@@ -5551,9 +5611,10 @@ extern "C" int farms_import_flows_async(farms_handle *h, const int32_t *d_idx, i
     hipStream_t sc = h->s_chain;
     HIPCHK(hipStreamWaitEvent(sc, w.ready, 0));
     Ctx c{};
-    c.t = f.t; c.evf = w.evf; c.valid = w.valid;
-    if (count > 0)
-        hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, sc, c, d_idx, (int)count, d_flows);
+    c.t = f.t; c.evf = w.evf; c.valid = w.valid; c.n = (int)f.n;
+    if (count > 0)  // (out-of-range indices skipped; counted in a word nobody reads: the call does not wait)
+        hipLaunchKernelGGL(k_import_flows, dim3(ceil_div(count, 256)), dim3(256), 0, sc, c, d_idx, (int)count, d_flows,
+                           h->err + 4);
     HIPCHK(hipEventRecord(w.ready, sc));
     HIPCHK(hipGetLastError());
     w.ready_host = false;  // (the pooling's chain waits w.ready: on its own stream, already in order)

@@ -160,7 +160,10 @@ int farms_process_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y
  * asynchronously under them; a farms_pool_device with no later fit pending
  * waits for the device.  Equivalent to farms_process_device when nothing is
  * imported.  Records of non-owned events are left unspecified; a halo flow
- * never imported counts as invalid. */
+ * never imported counts as invalid.  An index outside [0, n) is skipped (no
+ * device write through it); farms_export_flows / farms_export_wait and
+ * farms_import_flows then return FARMS_EINVAL (the asynchronous import does
+ * not wait, so it cannot report). */
 int farms_fit_device(farms_handle *h, const int32_t *d_x, const int32_t *d_y, const uint32_t *d_t_rel,
                      const int32_t *d_p, int64_t n, farms_records *d_out);
 int farms_export_flows(farms_handle *h, const int32_t *d_idx, int64_t count, double *d_flows);

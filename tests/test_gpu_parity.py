@@ -129,6 +129,38 @@ def test_short_wide_sensor_double_visits():
     assert rep["valid_ref"] > 1000
 
 
+@pytest.mark.parametrize("pairs", ["1", "0"])
+def test_short_wide_sensor_sparse_band_split_vs_oracle(pairs, monkeypatch):
+    """k_cand's band-contiguous slots on a short wide sensor (160 x 24, M = 50
+    > H): the W-1 clip carries every window row over three x-rows, so a row
+    can cross a column band (32 columns here) two x-rows past its start, not
+    only at the next one.  The row must split there: the slots between band
+    b's last candidate and band b+1's first are not band b's.  The stream is
+    sparse per pooling chunk (256-event chunks, ~10-30 % of the cells are
+    candidates) and its stamps are compressed 64x, so that the ring of three
+    candidate buffers (pool_batch 1) still holds contributors of a chunk three
+    back in those slots: a row read past its band's count pools them.  Both
+    pooling kernels (k_pool2 pairs, k_pool one event per wave) against the
+    oracle."""
+    W, H = 160, 24
+    n = 40_000
+    ev = farms.synth_config(1, n)
+    x = (ev.x.astype(np.int64) % W).astype(np.int32)
+    y = (ev.y.astype(np.int64) % H).astype(np.int32)
+    t = ((ev.t - ev.t[0]) // 64).astype(np.uint32)
+    p = np.maximum(ev.p, 0).astype(np.int32)
+    monkeypatch.setenv("FARMS_CAND", "events")
+    monkeypatch.setenv("FARMS_POOL_PAIRS", pairs)
+    with farms.FlowManager(H, W, 3, 3, pool_chunk=256, pool_batch=1) as fm:
+        g = fm.process(x, y, t, p)
+        info = fm.kernel_info()
+    assert info["cand_last"] == "k_cand", info
+    assert info["pool"].startswith("k_pool2<" if pairs == "1" else "k_pool<"), info
+    r, rc = oracles(x, y, t, p, H, W, 3, 3)
+    rep = assert_parity(g, r, H, W, rc=rc)
+    assert rep["valid_ref"] > 1000
+
+
 def test_three_scales_vs_oracle():
     """BASELINE config 5 shape: fs=7 with scales {0,25,50}, a 500k-event head."""
     ev = farms.synth_config(5, 500_000)
@@ -697,7 +729,11 @@ def test_async_exchange_order_is_bitwise(fs):
     scatter queued on the chain stream ahead of b's pooling.  Records bitwise
     farms_process; the exported flows bitwise those of one fit at a time with
     the synchronous farms_export_flows (the exchange calls act on the oldest
-    fit not yet pooled)."""
+    fit not yet pooled).  A second pass re-imports a subset of each sub-batch's
+    exported flows, every third with L = 0 (the event then counts as invalid),
+    through both orders: the scatter on the chain stream ahead of the pooling
+    takes effect (records differ from the plain run) and the two orders agree
+    bit for bit."""
     ev = farms.synth_config(4 if fs == 7 else 3, 200_000)
     x, y, t, p = ev.relative()
     with farms.FlowManager(720, 1280, fs, 5) as fm:
@@ -708,11 +744,26 @@ def test_async_exchange_order_is_bitwise(fs):
     splits = [(0, 50_000), (50_000, 50_001), (50_001, 120_000), (120_000, 160_000), (160_000, n)]
     none = torch.zeros(0, dtype=torch.int32, device=dev)
 
-    def run(async_order):
+    def imports(b, idx, bufs, reimport, keep):
+        """(indices, flows) to import after sub-batch b's export: none, or
+        every other exported slot with every third of those zeroed (kept
+        alive until the end: the engine reads them when the pooling runs)."""
+        if not reimport:
+            return none, bufs[b]
+        sel = torch.arange(0, len(idx[b]), 2, device=dev)
+        ii = idx[b][sel].contiguous()
+        fl = bufs[b][sel].clone()
+        fl[::3, 0] = 0.0
+        torch.cuda.current_stream().synchronize()  # both made on torch's stream: complete before the engine reads them
+        keep += [ii, fl]
+        return ii, fl
+
+    def run(async_order, reimport=False):
         o = {c: torch.zeros(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
              for c in farms.COLUMNS[4:]}
         idx = [torch.arange(0, b - a, 5, dtype=torch.int32, device=dev) for a, b in splits]
         bufs = [torch.full((len(i), 3), -1.0, dtype=torch.float64, device=dev) for i in idx]
+        keep = []
         with farms.FlowManager(720, 1280, fs, 5, fit_chunk=8192) as fm:
             def fit(b):
                 a, e = splits[b]
@@ -724,7 +775,7 @@ def test_async_exchange_order_is_bitwise(fs):
                     if nxt < len(splits):
                         fit(nxt)
                     fm.export_wait()
-                    fm.import_flows_async(none, bufs[b])
+                    fm.import_flows_async(*imports(b, idx, bufs, reimport, keep))
                 fit(0)
                 exchange(0, 1)
                 for b in range(len(splits)):
@@ -735,7 +786,7 @@ def test_async_exchange_order_is_bitwise(fs):
                 for b in range(len(splits)):
                     fit(b)
                     fm.export_flows(idx[b], bufs[b])
-                    fm.import_flows(none, bufs[b])
+                    fm.import_flows(*imports(b, idx, bufs, reimport, keep))
                     fm.pool_device()
             torch.cuda.synchronize()
         g = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
@@ -749,3 +800,36 @@ def test_async_exchange_order_is_bitwise(fs):
     for a, b in zip(f_async, f_sync):
         assert a.tobytes() == b.tobytes()
         assert (a[:, 0] >= 0).all()  # every slot written
+    r_async, _ = run(True, reimport=True)
+    r_sync, _ = run(False, reimport=True)
+    assert bitwise_equal(r_async, r_sync), compare(r_sync, r_async)
+    assert not bitwise_equal(ref, r_sync)  # the zeroed flows took effect
+
+
+def test_exchange_index_outside_the_fit_is_refused():
+    """farms_export_flows / farms_import_flows with an index outside the fit's
+    events: nothing is read or written through it (no device fault) and the
+    synchronous calls return FARMS_EINVAL; the handle then pools as usual."""
+    ev = farms.synth_config(2, 20_000)
+    x, y, t, p = ev.relative()
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (x, y, t.view(np.int32), p)]
+    n = len(x)
+    o = {c: torch.zeros(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+         for c in farms.COLUMNS[4:]}
+    with farms.FlowManager(320, 320, 5, 5) as fm:
+        ref = fm.process(x, y, t, p)
+        fm.reset()
+        fm.fit_device(*d, o)
+        bad = torch.tensor([0, n, -1, 1 << 30], dtype=torch.int32, device=dev)
+        buf = torch.full((4, 3), -7.0, dtype=torch.float64, device=dev)
+        torch.cuda.current_stream().synchronize()  # (made on torch's stream)
+        for call in (lambda: fm.export_flows(bad, buf), lambda: fm.import_flows(bad[1:], buf[1:])):
+            with pytest.raises(farms.FarmsError) as ei:
+                call()
+            assert ei.value.code == farms.FARMS_EINVAL
+        assert (buf[1:] == -7.0).all() and (buf[0] >= 0).all()  # only the valid slot written
+        fm.pool_device()
+    g = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
+    g.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
+    assert bitwise_equal(ref, g), compare(ref, g)

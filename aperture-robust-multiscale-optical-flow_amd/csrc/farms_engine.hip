@@ -416,6 +416,29 @@ __global__ void k_validate(const int32_t *x, const int32_t *y, int n, int x0, in
     if (ex < x0 || ex >= x1 || ey < 0 || ey >= H) atomicOr(err, 1);
 }
 
+// Several device fills in one launch (farms_reset: the SAE, flow snapshots,
+// per-set cursors and counters were thirteen hipMemsetAsync launches, about
+// 0.1 ms of a 3.3-ms C2 step): segment i is words[i] 32-bit words of pattern
+// pat[i] from p[i] (16-B aligned, as hipMalloc returns), stored 16 B at a time.
+constexpr int kFillSegs = 16;
+struct FillTable {
+    void *p[kFillSegs];
+    int64_t words[kFillSegs];
+    uint32_t pat[kFillSegs];
+    int n;
+};
+__global__ void k_fill(FillTable t) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < t.n; ++k) {
+        const uint32_t v = t.pat[k];
+        uint4 *q = static_cast<uint4 *>(t.p[k]);
+        const int64_t nq = t.words[k] >> 2;
+        for (int64_t i = i0; i < nq; i += st) q[i] = make_uint4(v, v, v, v);
+        uint32_t *w = static_cast<uint32_t *>(t.p[k]);
+        for (int64_t i = 4 * nq + i0; i < t.words[k]; i += st) w[i] = v;
+    }
+}
+
 // Per position k of P (events sorted by pixel, then index): PT[k] = {event,
 // stamp}, and the event's link record, one 16-B scatter per event.  The stamp
 // of the previous position comes from the neighbouring lane.
@@ -500,14 +523,19 @@ __device__ __forceinline__ void fit_prep_thread(const Ctx &c, SaeBuf cells, int 
         else vis = hd->w & kHeadVisited;  // no earlier event in this call: keep the snapshot of earlier calls
         hd->w = vis | kHeadTouched | (nx < c1 ? kHeadMore : 0u) | (uint32_t)e;
         hd->t1 = c.t[e];
-        tl->run_lo = lk.x;
+        // the tail is read only for a pixel that fires more than once in the
+        // chunk (kHeadMore), and its run bounds only past a second event: a
+        // pixel that fires once (84 % of them in fs 7's 65,536-event chunks)
+        // leaves its tail's line untouched (scattered partial-line writes were
+        // most of the prep's HBM traffic, 7.2 of 9.9 MB per C4 launch)
         if (nx < c1) {  // and the second one
             const int nn = c.link[nx].z;
             tl->e2m = (uint32_t)nx | (nn < c1 ? 0x80000000u : 0u);
             tl->t2 = c.t[nx];
+            tl->run_lo = lk.x;
         }
     }
-    if (nx >= c1) cells.tail[q].run_hi = lk.x;
+    if (nx >= c1 && lk.y >= c0) cells.tail[q].run_hi = lk.x;  // the last of two or more
 }
 
 // Pooling descriptors of work-order positions [p0, p1): {event, x, y, t}, the
@@ -4196,7 +4224,9 @@ struct farms_handle {
     int tile_bits = 0;
     int tile_shift = 3;       // work-order tile: 2^tile_shift square
     int *err = nullptr;       // device words: [0] range check, [1] k_prep, [2] export / [3] import index check, [4] async import
-    int *err_pin = nullptr;   // pinned host copies of those words
+    int *err_pin = nullptr;   // pinned host copies of those words ([5]: the range check's)
+    hipEvent_t val_ev = nullptr;  // the range check's result in err_pin[5] (s_copy)
+    bool val_pending = false;     // ... not yet looked at: before the call's first fit (check_valid)
     unsigned long long *counters = nullptr;
     bool profiling = false;  // kernel timing events
     bool counting = false;   // work counters (k_stats, per-event candidate counts)
@@ -4408,8 +4438,7 @@ int clear_stats(farms_handle *h) {
     std::sort(h->ev_free.begin(), h->ev_free.end());
     h->ev_free.erase(std::unique(h->ev_free.begin(), h->ev_free.end()), h->ev_free.end());
     h->acc = farms_stats{};
-    h->counters_dirty = false;
-    HIPCHK(hipMemset(h->counters, 0, sizeof(unsigned long long) * 8));
+    h->counters_dirty = false;  // (the device counters: zeroed by reset_surfaces' fill)
     return FARMS_OK;
 }
 
@@ -4418,16 +4447,26 @@ int reset_surfaces(farms_handle *h) {
     if (rc) return rc;
     // tag 0: never visited, never touched (chunk seqs start at 1)
     // both SAE buffers, each WH cells and a guard head (index WH, never written:
-    // the fit reads it for cells outside the stored region)
-    HIPCHK(hipMemsetAsync(h->sae_head, 0, 2 * sizeof(SaeHead) * (h->WH + 1), h->stream));
-    HIPCHK(hipMemsetAsync(h->sae_tail, 0, 2 * sizeof(SaeTail) * (h->WH + 1), h->stream));
-    HIPCHK(hipMemsetAsync(h->ftime, 0xFF, sizeof(int64_t) * h->WH, h->stream));   // -1: no valid flow
-    HIPCHK(hipMemsetAsync(h->fsnap, 0, sizeof(FlowCell) * h->WH, h->stream));
+    // the fit reads it for cells outside the stored region); every fill in one
+    // launch (k_fill)
+    FillTable ft{};
+    auto fill = [&](void *ptr, size_t bytes, uint32_t pat) {
+        ft.p[ft.n] = ptr;
+        ft.words[ft.n] = (int64_t)(bytes / 4);
+        ft.pat[ft.n] = pat;
+        ++ft.n;
+    };
+    fill(h->sae_head, 2 * sizeof(SaeHead) * (h->WH + 1), 0u);
+    fill(h->sae_tail, 2 * sizeof(SaeTail) * (h->WH + 1), 0u);
+    fill(h->ftime, sizeof(int64_t) * h->WH, 0xFFFFFFFFu);  // -1: no valid flow
+    fill(h->fsnap, sizeof(FlowCell) * h->WH, 0u);
     for (Work &w : h->ws) {
-        HIPCHK(hipMemsetAsync(w.pcur, 0, sizeof(int32_t) * h->WH, h->stream));
-        HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, h->stream));
-        HIPCHK(hipMemsetAsync(w.cinfo, 0, sizeof(int) * kCiWords, h->stream));
+        fill(w.pcur, sizeof(int32_t) * h->WH, 0u);
+        fill(w.pend, sizeof(int32_t) * h->WH, 0xFFFFFFFFu);
+        fill(w.cinfo, sizeof(int) * kCiWords, 0u);
     }
+    fill(h->counters, sizeof(unsigned long long) * 8, 0u);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, h->stream, ft);
     HIPCHK(hipStreamSynchronize(h->stream));
     if ((rc = clear_stats(h))) return rc;
     h->seq = 0;
@@ -4476,10 +4515,29 @@ void launch_pool2(const Ctx &c, int ch0, int ch1, const int32_t *nv, int4 *ovf, 
     const size_t lds = sizeof(uint64_t) * 2 * (size_t)pair_half_words(pair_bw(c.pool_bw), c.pool_rs);
     hipLaunchKernelGGL((k_pool2<K, W7>), dim3((ch1 - ch0) * (c.C2 >> 1)), dim3(64), lds, s, c, ch0, ch1, nv, ovf,
                        ovfn);
+}
+// The overflow list of a k_pool2 launch (events past the pair bitmap), pooled
+// one event per wave right after it on the pooling stream.  (On the chain
+// stream instead, ahead of k_true_polar, its pooling-sized waves waited for
+// slots beside the pooling and held the next super-chunk's candidate build:
+// C2 2.95 -> 4.8 ms per call, profiles/r06_ab_ovf_stream_c2.log.)
+template <int K, bool W7>
+void launch_pool_ovf(const Ctx &c, const int4 *ovf, const int *ovfn, hipStream_t s) {
     const size_t lds1 = sizeof(uint64_t) * (size_t)(c.pool_bw + c.pool_rs + kPoolValWords);
     hipLaunchKernelGGL((k_pool_ovf<K, W7>), dim3(kPoolOvfBlocks), dim3(64), lds1, s, c, ovf, ovfn);
 }
 typedef void (*pair_launcher)(const Ctx &, int, int, const int32_t *, int4 *, int *, hipStream_t);
+typedef void (*ovf_launcher)(const Ctx &, const int4 *, const int *, hipStream_t);
+template <bool W7>
+ovf_launcher ovf_for_cap(int K) {
+    switch (K) {
+    case 2: return launch_pool_ovf<2, W7>;   case 3: return launch_pool_ovf<3, W7>;   case 4: return launch_pool_ovf<4, W7>;
+    case 5: return launch_pool_ovf<5, W7>;   case 6: return launch_pool_ovf<6, W7>;   case 7: return launch_pool_ovf<7, W7>;
+    case 8: return launch_pool_ovf<8, W7>;   case 9: return launch_pool_ovf<9, W7>;   case 10: return launch_pool_ovf<10, W7>;
+    case 11: return launch_pool_ovf<11, W7>;
+    default: return nullptr;
+    }
+}
 template <bool W7>
 pair_launcher pair_for_cap(int K) {
     switch (K) {
@@ -4504,6 +4562,7 @@ pair_launcher pair_for(int K, int fr, int pool_chunk) {
     if (!on || (pool_chunk & 1)) return nullptr;
     return pool_w7(fr) ? pair_for_cap<true>(K) : pair_for_cap<false>(K);
 }
+ovf_launcher ovf_for(int K, int fr) { return pool_w7(fr) ? ovf_for_cap<true>(K) : ovf_for_cap<false>(K); }
 // Tuning knobs of the fit (A/B aids; every choice gives the same bits):
 // FARMS_FIT_QUAD=0: one thread per event; FARMS_FIT_MODE 0 = re-gather the
 // winning window, 1 = union tile with columns per lane (default), 2 = union
@@ -4682,13 +4741,16 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
         // of b + 2 is issued under the fit of b + 1, that is the host's one
         // wait per sub-batch (profiles/r05_strips_async_c4.log; the fits of
         // two-phase calls on stream F alone instead: 99.7 against 77.2 ms)
+        // The prep below touches only the workspace set (k_prep clamps a bad
+        // event's pixel to 0), so it is enqueued at once and the host waits
+        // for the check only before the first fit writes the SAE (check_valid,
+        // run_core): the sort and links run under the host's round trip.
         hipStream_t sv = h->s_copy;
-        int herr = 0;
         HIPCHK(hipMemsetAsync(h->err, 0, sizeof(int), sv));
         hipLaunchKernelGGL(k_validate, dim3(ceil_div(n, 256)), dim3(256), 0, sv, c.x, c.y, n, c.X0, c.XR1, c.H, h->err);
-        HIPCHK(hipMemcpyAsync(&herr, h->err, sizeof(int), hipMemcpyDeviceToHost, sv));
-        HIPCHK(hipStreamSynchronize(sv));
-        if (herr) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+        HIPCHK(hipMemcpyAsync(h->err_pin + 5, h->err, sizeof(int), hipMemcpyDeviceToHost, sv));
+        HIPCHK(hipEventRecord(h->val_ev, sv));
+        h->val_pending = true;
     }
     // (k_prep's own flag goes to the second word: the events are in range here)
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err + 1,
@@ -4826,6 +4888,9 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     // its k_pool is done; then its records are final (round 4: k_true_polar
     // off the pooling stream, which paces the step at C3; the chain stream,
     // one super-chunk ahead, has the slack)
+    pool_launcher pl = pool_for(h->K, h->fr);
+    pair_launcher pl2 = pair_for(h->K, h->fr, h->pool_chunk);
+    ovf_launcher plo = pl2 ? ovf_for(h->K, h->fr) : nullptr;
     auto finish_super = [&](int T) -> int {
         const int q0 = T * B * h->pool_chunk, q1 = super_end(T);
         HIPCHK(hipStreamWaitEvent(sc, ev_pk(T), 0));
@@ -4837,8 +4902,6 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         }
         return FARMS_OK;
     };
-    pool_launcher pl = pool_for(h->K, h->fr);
-    pair_launcher pl2 = pair_for(h->K, h->fr, h->pool_chunk);
     const bool fast_fit = h->fr >= 1 && h->fr <= 3;
     const bool fit_quad = fit_quad_env();
     const int fit_mode = fit_mode_env();
@@ -4878,6 +4941,11 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         hipLaunchKernelGGL(k_fit_prep, dim3(pr.blocks), dim3(64), 0, st, c, pr.cells, pr.p0, pr.c0, pr.c1, pr.seq);
     };
     auto enqueue_fit = [&](int f) -> int {  // fit chunk f on stream F (or F2)
+        if (h->val_pending) {  // the call's range check (enqueue_prep), before anything writes the SAE
+            h->val_pending = false;
+            HIPCHK(hipEventSynchronize(h->val_ev));
+            if (h->err_pin[5]) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+        }
         const int c0 = fit_start(f), c1 = fit_chunk_end(f);
         hipStream_t sf = fit_stream(f);
         if (two && f == 1) HIPCHK(hipStreamWaitEvent(sf, w.sync_ev[0], 0));  // F2 starts behind the call's prep
@@ -5020,7 +5088,10 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
         const int p0 = ch0 * h->pool_chunk, p1 = (int)std::min<int64_t>((int64_t)ch1 * h->pool_chunk, n);
         hipEvent_t k0 = nullptr, k1 = nullptr;
         if (prof) { int rc = mark(h, sp, &k0); if (rc) return rc; }
-        if (pl2) pl2(c, ch0, ch1, w.nv, w.ovf + (int64_t)ch0 * h->pool_chunk, w.ovfn + S, sp);
+        if (pl2) {  // the pairs, then their overflow list (events past the pair bitmap)
+            pl2(c, ch0, ch1, w.nv, w.ovf + (int64_t)ch0 * h->pool_chunk, w.ovfn + S, sp);
+            plo(c, w.ovf + (int64_t)ch0 * h->pool_chunk, w.ovfn + S, sp);
+        }
         else pl(c, p0, p1, sp);
         if (prof) {
             int rc = mark(h, sp, &k1);
@@ -5224,7 +5295,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         hipStreamCreateWithPriority(&h->s_copy, hipStreamNonBlocking, prio_hi) != hipSuccess)  // (device calls: odd fits)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {
-        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->ex_ev};
+        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->ex_ev, &h->val_ev};
         for (Work &w : h->ws) {
             evs.push_back(&w.done);
             evs.push_back(&w.ready);
@@ -5277,6 +5348,7 @@ extern "C" int farms_destroy(farms_handle *h) {
         if (ev) (void)hipEventDestroy(ev);
     if (h->chain_end) (void)hipEventDestroy(h->chain_end);
     if (h->ex_ev) (void)hipEventDestroy(h->ex_ev);
+    if (h->val_ev) (void)hipEventDestroy(h->val_ev);
     if (h->last_buf) (void)hipFree(h->last_buf);
     dfree(h->bw_ring); dfree(h->cscr);
     dfree(h->hdr_ring); dfree(h->val_ring); dfree(h->err); dfree(h->counters);

@@ -71,9 +71,10 @@ def parse():
                     help="N > 1: events per rank of the short stream whose merged records are checked against "
                          "the oracle before the timed steps (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split", choices=multirank.SPLITS, default="segments",
+    ap.add_argument("--split", choices=multirank.SPLITS, default=None,
                     help="N > 1: temporal segments (time-ordered streams), x-strips with an RCCL exchange of "
-                         "halo flows, or x-strips that recompute their halos")
+                         "halo flows, or x-strips that recompute their halos.  Default: x-strips for configs 4 "
+                         "and 5 (BASELINE's 4- / 8-tile spatial partition with a border halo), segments otherwise")
     ap.add_argument("--host-steps", type=int, default=2,
                     help="N=1: steps of the host-array path (farms_process: H2D + kernels + D2H) timed after "
                          "the device-resident ones (0 = skip)")
@@ -86,7 +87,28 @@ def parse():
     ap.add_argument("--plan-only", action="store_true",
                     help="launch, rendezvous, per-rank stream shares and partition only; no GPU, no timing "
                          "(CPU test of the multi-rank plumbing; value is null)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.split is None:
+        a.split = default_split(a.config)
+    return a
+
+
+def default_split(cfg: int) -> str:
+    """BASELINE configs 4 and 5 state a spatial partition ("4-tile spatial
+    partition with RCCL border halo", "8-tile partition"): their multi-GPU lines
+    run the x-strips with the halo-flow exchange.  The other configs state one
+    GPU; their N > 1 lines run temporal segments (the better-scaling split,
+    DESIGN.md §6), named as such in config.workload."""
+    return "strips" if cfg in (4, 5) else "segments"
+
+
+def split_name(split: str, world: int) -> str:
+    """The partition a line measured, as config.workload names it."""
+    if world == 1:
+        return "1 GPU"
+    return {"strips": f"{world}-tile spatial partition (x-strips) with RCCL halo-flow exchange",
+            "strips-recompute": f"{world}-tile spatial partition (x-strips), halos recomputed, no collective",
+            "segments": f"{world} temporal segments (not a spatial partition), RCCL all-gather of SAE surfaces"}[split]
 
 
 def free_port() -> int:
@@ -388,7 +410,8 @@ def main():
             dist.all_reduce(tt)
             total = int(tt.item())
         line = {"metric": METRIC, "value": None, "unit": "Mevents/s", "n_gpus": world, "plan_only": True,
-                "config": {"workload": f"BASELINE config {cfg}", "events_per_gpu": per_gpu, "parallelism": sh.label},
+                "config": {"workload": f"BASELINE config {cfg}; {split_name(args.split, world)}",
+                           "split": args.split, "events_per_gpu": per_gpu, "parallelism": sh.label},
                 "detail": {"owned_events_all_ranks": total, "stream_events": sh.n_stream,
                            "rank0_stored_events": n, "rank0_owned_events": n_owned}}
         if rank == 0:
@@ -483,7 +506,9 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"BASELINE config {cfg}: {W}x{H} synthetic moving-bars stream, "
-                               f"{per_gpu} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}",
+                               f"{per_gpu} events/GPU, filtersize {fs}, inlierCheck 5, scales 0..{maxw} step {jump}; "
+                               f"{split_name(args.split, world)}",
+                   "split": args.split if world > 1 else "none",
                    "events_per_gpu": per_gpu, "width": W, "height": H, "filtersize": fs,
                    "parallelism": sh.label},
         "roofline": roofline,

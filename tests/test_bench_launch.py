@@ -40,6 +40,18 @@ def test_gpus_2_launches_two_ranks(split):
     assert d["detail"]["rank0_owned_events"] < 120000
 
 
+@pytest.mark.parametrize("cfg,want", [(2, "segments"), (4, "strips"), (5, "strips")])
+def test_default_split_follows_the_baseline_partition(cfg, want):
+    """BASELINE configs 4 and 5 state a spatial partition with a border halo:
+    their N > 1 lines default to the x-strips; the one-GPU configs' N > 1
+    lines run temporal segments.  config.workload names the split either way."""
+    r = run_bench("--gpus", "2", "--plan-only", "--config", str(cfg), "--events", "60000")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = last_json(r.stdout)
+    assert d["config"]["split"] == want
+    assert ("-tile spatial partition" in d["config"]["workload"]) == (want == "strips")
+
+
 def test_world_size_must_match_gpus():
     r = run_bench("--gpus", "1", "--plan-only", env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

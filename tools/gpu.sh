@@ -7,6 +7,7 @@
 #   tools/gpu.sh TAG ab CONFIG STEPS LIB...     tools/lib_ab.py: builds side by side, alternating
 #   tools/gpu.sh TAG stats [BENCH ARGS...]      rocprofv3 --kernel-trace --stats of a bench run
 #   tools/gpu.sh TAG serial [BENCH ARGS...]     FARMS_SERIALIZE=1 kernel timeline (no overlap)
+#   tools/gpu.sh TAG trace [BENCH ARGS...]      kernel trace of one bench step, tools/trace_gaps.py summary
 #   tools/gpu.sh TAG sq [BENCH ARGS...]         one --pmc pass of 8 SQ counters -> TAG_sq.json
 #   tools/gpu.sh TAG traffic [BENCH ARGS...]    FETCH_SIZE / WRITE_SIZE passes -> TAG_traffic.json
 #   tools/gpu.sh TAG ranksim [strip_rank.py ARGS...]
@@ -44,6 +45,11 @@ serial)
     python3 bench.py $PROF_ARGS "$@" > $O.log 2>&1
   rc=$?
   if [ $rc -eq 0 ]; then python3 tools/timeline.py $O/kt_kernel_trace.csv > $O.txt; rc=$?; grep -E "span|busy|k_|rocprim" $O.txt | head -20 || true; fi ;;
+trace)
+  timeout -k 10 400 rocprofv3 --kernel-trace -d $O -o kt --output-format csv -- \
+    python3 bench.py $PROF_ARGS "$@" > $O.log 2>&1
+  rc=$?
+  if [ $rc -eq 0 ]; then python3 tools/trace_gaps.py $O/kt_kernel_trace.csv --call ${CALL:-0} > $O.txt; rc=$?; head -40 $O.txt; fi ;;
 sq)
   CTRS="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD"
   timeout -s KILL 600 rocprofv3 --pmc $CTRS --kernel-include-regex "$KREGEX" -d $O -o pmc --output-format csv -- \

@@ -5826,7 +5826,22 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         if (n > 2 * per) sub = per;
     }
     if (sub > kMaxCallEvents) sub = std::max<int64_t>(kMaxCallEvents / super, 1) * super;  // event ids of a sub-batch: 29 bits
-    const int nbat = ceil_div(n, sub);
+    // Sub-batch bounds.  The first sub-batches grow from two super-chunks by 4x
+    // up to `sub`: the call's head (the first sub-batch's range check and
+    // upload, not hidden by compute: ~2.5 ms at C3 with n / 8) shrinks, and each
+    // later upload still hides under the compute of the one before it (an
+    // event uploads ~4.7x faster than it computes at C3).  FARMS_SUB_HEAD=0:
+    // equal sub-batches (A/B aid; the records are the same either way).
+    std::vector<int64_t> bnd{0};
+    {
+        const char *shv = getenv("FARMS_SUB_HEAD");
+        int64_t size = (shv && shv[0] == '0') ? sub : std::min<int64_t>(2 * super, sub);
+        while (bnd.back() < n) {
+            bnd.push_back(std::min<int64_t>(n, bnd.back() + size));
+            size = std::min<int64_t>(4 * size, sub);
+        }
+    }
+    const int nbat = (int)bnd.size() - 1;
     int rc = FARMS_OK;
     for (int k = 0; k < std::min(nbat, 2) && !rc; ++k) rc = ensure_capacity(h, h->ws[k], sub);  // set b % 2
     if (!rc) rc = ensure_io(h, n);
@@ -5872,7 +5887,8 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     // one completion event per pooling super-chunk of the call, created before
     // the copy-out threads start: the hook must not grow copy_ev while they read it
     {
-        const int64_t n_super_all = (int64_t)nbat * ceil_div(ceil_div(sub, h->pool_chunk), h->pool_batch);
+        int64_t n_super_all = 0;
+        for (int k = 0; k < nbat; ++k) n_super_all += ceil_div(ceil_div(bnd[k + 1] - bnd[k], h->pool_chunk), h->pool_batch);
         while ((int64_t)h->copy_ev.size() < n_super_all) {
             hipEvent_t ev;
             HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -5996,7 +6012,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     // range check (vFlow.cpp:264 indexes the surfaces unchecked), staging and
     // upload of sub-batch b into the call's device copies (nothing to wait for)
     auto upload = [&](int b) -> int {
-        const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
+        const int64_t a0 = bnd[b], m = bnd[b + 1] - a0;
         std::atomic<int> oor{0};
         host_parallel(m, T, [&](int64_t i0, int64_t i1) {
             const int64_t e0 = a0 + i0, k = i1 - i0;
@@ -6027,7 +6043,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     };
     int uploaded = 0;
     for (int b = 0; b < nbat && !rc; ++b) {
-        const int64_t a0 = (int64_t)b * sub, m = std::min<int64_t>(sub, n - a0);
+        const int64_t a0 = bnd[b], m = bnd[b + 1] - a0;
         Work &w = h->ws[b & 1];
         // (pinned inputs uploaded all up front: 1.5 ms slower at C3, the burst of
         // uploads slows the first sub-batches' kernels more)

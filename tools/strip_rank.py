@@ -36,6 +36,7 @@ ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--events", type=int, default=50_000_000, help="events per GPU")
 ap.add_argument("--nsub", type=int, default=8, help="strips: sub-batches of the pipelined step")
 ap.add_argument("--pool", type=int, default=0, help="pooling chunk (0: the engine's default)")
+ap.add_argument("--fit-chunk", type=int, default=0, help="fit chunk (0: the engine's default)")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--split", choices=multirank.SPLITS, default="strips")
 ap.add_argument("--host-times", action="store_true",
@@ -71,7 +72,7 @@ for r in ranks:
     out = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
            for c in farms.COLUMNS[4:]}
     fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=maxw, pool_chunk=a.pool,
-                           **multirank.engine_args(sh))
+                           fit_chunk=a.fit_chunk, **multirank.engine_args(sh))
     if sh.lists is not None:
         s = sh.strip
         # realistic halo flows: a handle that fits the whole stored region itself

@@ -2710,6 +2710,13 @@ __device__ __forceinline__ double wave_max(double v) {
 // masked fma, fma(v, m, acc) with m in {0, 1}, is bitwise equal -- acc starts
 // at +0 and a round-to-nearest sum is -0 only when both addends are -- but
 // costs a compare, a select and an fma per entry.)
+// The scalar-mask folds below set exec to masks computed from scratch, valid
+// only under a full exec at entry; -DFARMS_CHECK_EXEC traps on any other.
+__device__ __forceinline__ void fold_exec_check() {
+#ifdef FARMS_CHECK_EXEC
+    if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
+}
 __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_t kw1, const double (&v)[8]) {
     uint64_t m0, m1, m2, m3, m4, m5, m6, m7, sv;
     asm volatile(
@@ -2751,9 +2758,13 @@ __device__ __forceinline__ void fold8(double &acc, int kk, uint32_t kw0, uint32_
 // The fold's only VALU instructions are then the exec-masked v_add_f64s (the
 // v_cmp per entry was about 157 of k_pool's ~1,115 VALU instructions per valid
 // event at C3, round 4).  Bitwise the fold8 sums: the same adds on the same
-// lanes.  Called with a full exec (wave-uniform control flow): the masks are
-// not intersected with it.  The shifts write SCC, hence the clobber.
+// lanes.  The shifted masks are NOT intersected with the exec at entry: every
+// caller runs with a full exec (wave-uniform control flow), which
+// fold_exec_check asserts in a -DFARMS_CHECK_EXEC build.  (Intersecting them,
+// one s_and_b64 before each add, measured C3 69.2 against 66.7 ms: the exec
+// write sits on the add chain.)  The shifts write SCC, hence the clobber.
 __device__ __forceinline__ void fold8_salu(double &acc, uint32_t sw0, uint32_t sw1, const double (&v)[8]) {
+    fold_exec_check();
     uint64_t sv;
     uint32_t t;
     asm volatile(
@@ -3507,9 +3518,11 @@ __device__ __forceinline__ int pool_rows2(const Ctx &c, int buf, int lane, bool 
 // lanes of A's half selected by byte u of a0:a1 (lanes >= 3 (k0 - 1) of the
 // half: the scales containing the entry; 30: padding, the half's junk lanes)
 // and B's likewise from b0:b1 (exec_lo, exec_hi), one v_add_f64 for both.  As
-// fold8_salu: a full exec at entry, SCC clobbered, exec restored.
+// fold8_salu: a full exec at entry (fold_exec_check), SCC clobbered, exec
+// restored.
 __device__ __forceinline__ void fold8_pair(double &acc, uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1,
                                            const double (&v)[8]) {
+    fold_exec_check();
     uint64_t sv;
     uint32_t ta, tb;
 #define FARMS_PAIR_SLOT(WA, WB, SH, V)                                                             \

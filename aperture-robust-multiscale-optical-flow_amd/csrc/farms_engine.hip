@@ -80,7 +80,7 @@ constexpr double kTsToSec = 1e-6;           // vFlow.h:28
 constexpr double kKillUs = 500.0;           // vFlow.cpp:961
 constexpr int kDefaultFitChunk = 1 << 16;
 constexpr int kDefaultPoolChunk = 1 << 13;
-constexpr int kDefaultPoolBatch = 64;  // pooling chunks per super-chunk (ring of 2B+1 candidate buffers)
+constexpr int kDefaultPoolBatch = 64;  // pooling chunks per super-chunk (ring of 3B+1 candidate buffers)
 constexpr int kMaxScales = 16;
 
 // Local-flow state of one event, and the flow surface cell (x-major).  L = 0 for
@@ -4188,9 +4188,10 @@ struct farms_handle {
     SaeTail *sae_tail = nullptr;  // two of WH + 1 tails
     int64_t *ftime = nullptr;
     FlowCell *fsnap = nullptr;
-    // ring of per-chunk candidate buffers (NB = 2 x pool_batch + 1), indexed by
-    // the chunk's number since the last reset (calls continue the ring)
-    int pool_batch = kDefaultPoolBatch, NB = 2 * kDefaultPoolBatch + 1;
+    // ring of per-chunk candidate buffers (NB = 3 x pool_batch + 1), indexed by
+    // the chunk's number since the last reset (calls continue the ring): the
+    // candidate build of super-chunk S overwrites only buffers of S - 3
+    int pool_batch = kDefaultPoolBatch, NB = 3 * kDefaultPoolBatch + 1;
     BmWord *bw_ring = nullptr;
     int nblk = 0;
     int64_t cstride = 0;
@@ -4203,7 +4204,7 @@ struct farms_handle {
     int cand_last = -1;           // the last pooling call's candidate build: 1 k_cand, 0 k_chain
     int *plan_pin = nullptr;      // pinned: kCiMaxBack of each workspace set's last prep
     int64_t chunk_base = 0, super_base = 0;  // pooling chunks / super-chunks enqueued since the last reset
-    hipEvent_t gpool[3] = {};                // pooling done of the last super-chunks (by number % 3)
+    hipEvent_t gpool[4] = {};                // pooling done of the last super-chunks (by number % 4)
     hipEvent_t chain_end = nullptr;          // the last call's candidate chain done
     hipEvent_t ex_ev = nullptr;              // farms_export_flows_async: its gather done (stream F)
     void *last_buf = nullptr;                // farms_last_stamps: tile counts and event buckets (grown on demand)
@@ -4646,6 +4647,40 @@ bool launch_fit(const Ctx &c, int fr, int c0, int c1, uint32_t seq, hipStream_t 
 }
 
 
+// FARMS_PLAN_CHECK=1 (test aid): a call with a host-side plan (cand_hint) also
+// waits for the device's and fails on a difference.
+bool plan_check() {
+    const char *v = getenv("FARMS_PLAN_CHECK");
+    return v && v[0] == '1';
+}
+
+// The candidate plan's reach (k_cand_plan_max / k_cand_plan_back, restated on
+// the host): the chunks' min / max stamps tmin / tmax in stream order; for each
+// chunk, the distance back to the first earlier chunk whose prefix-maximum
+// last stamp lies inside its kill window; the largest such distance.
+int host_plan_reach(const std::vector<uint32_t> &tmin, const std::vector<uint32_t> &tmax) {
+    const int nch = (int)tmin.size();
+    std::vector<uint32_t> pmax(nch);
+    uint32_t run = 0;
+    for (int i = 0; i < nch; ++i) pmax[i] = run = std::max(run, tmax[i]);
+    int reach = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+        const int64_t lo = (int64_t)tmin[ch] - (int64_t)kKillUs;
+        const int a = (int)(std::upper_bound(pmax.begin(), pmax.begin() + ch, lo,
+                                             [](int64_t v, uint32_t m) { return (int64_t)m > v; }) -
+                            pmax.begin());
+        reach = std::max(reach, ch - a);
+    }
+    return reach;
+}
+
+// FARMS_FINISH_LAG (A/B aid): 1 finishes super-chunk S - 1 behind the chain's
+// work for S (the round-5 order), 2 (default) S - 2; the ring (3B + 1) holds either.
+int finish_lag() {
+    const char *v = getenv("FARMS_FINISH_LAG");
+    return v && v[0] == '1' ? 1 : 2;
+}
+
 int ensure_sync_events(Work &w, size_t count) {
     while (w.sync_ev.size() < count) {
         hipEvent_t ev;
@@ -4843,13 +4878,13 @@ int record_pool_done(farms_handle *h, hipStream_t s, int64_t Sg, hipEvent_t ev) 
         return fail(FARMS_EINTERNAL, "pooling super-chunk " + std::to_string(Sg) +
                                          " marked done before its k_true_polar on the same stream");
     HIPCHK(hipEventRecord(ev, s));
-    HIPCHK(hipEventRecord(h->gpool[Sg % 3], s));
+    HIPCHK(hipEventRecord(h->gpool[Sg % 4], s));
     return FARMS_OK;
 }
 
 int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, const uint32_t *dt, const int32_t *dp,
              int64_t n64, farms_records *dout, const super_hook *on_super = nullptr, int phase = 0,
-             bool async = false, bool validated = false) {
+             bool async = false, bool validated = false, int cand_hint = -1) {
     const int n = (int)n64;
     hipStream_t s = h->stream;
     h->fresh = false;
@@ -4887,7 +4922,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     //   stream F: local plane fits, chunk after chunk (k_fit_prep, k_fit,
     //     or k_fit_wave for filters without a compile-time fast path);
     //   stream C: the candidate chain, one k_chain per pooling chunk, each
-    //     chunk's records into ring buffer (chunk number) % NB (NB = 2B + 1);
+    //     chunk's records into ring buffer (chunk number) % NB (NB = 3B + 1);
     //   stream P: one k_pool per super-chunk of B pooling chunks.
     // Pooling of a chunk reads only its candidate buffer, the per-event flows
     // and P, so it overlaps the chain of later chunks and the fit sweep.
@@ -5010,7 +5045,11 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     hipEvent_t t_pool0 = nullptr;  // the pooling sweep's start: the chain stream past the prep (phase 2: the fits)
     if (prof && phase != 1) { int rc = mark(h, sc, &t_pool0); if (rc) return rc; }
     // the candidate build of the call (k_cand / k_chain), decided on the host
-    // from the plan once the first super-chunk's fits are enqueued
+    // from the plan once the first super-chunk's fits are enqueued: the
+    // device's plan (a wait for the prep), or cand_hint, the same plan from the
+    // host's copy of the stamps (host_plan_reach: the host-array path, whose
+    // sub-batches would otherwise each wait for their prep behind the fits of
+    // the one before)
     int use_cand = -1;
     auto decide_cand = [&]() -> int {
         const int force = cand_force();
@@ -5018,9 +5057,13 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             use_cand = 0;
         } else if (force) {
             use_cand = force == 1;
+        } else if (cand_hint >= 0 && !plan_check()) {
+            use_cand = cand_hint;
         } else {
             HIPCHK(hipEventSynchronize(w.plan_ev));
             use_cand = h->plan_pin[&w - h->ws] <= kCandMaxBack;
+            if (cand_hint >= 0 && cand_hint != use_cand)
+                return fail(FARMS_EINTERNAL, "host candidate plan differs from the device's");
         }
         h->cand_last = use_cand;
         c.band_slots = use_cand ? 1 : 0;  // (the pooling launches below take c by value)
@@ -5051,6 +5094,7 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
     }
     if (phase == 2) fit_enqueued = n_fit_chunks;  // fits done (phase 1)
     const int64_t sb = h->super_base;  // global number of this call's first super-chunk
+    const int lag = finish_lag();      // super-chunks between a pooling launch and its k_true_polar
     for (int S = 0; S < n_super; ++S) {
         const int ch0 = S * B, ch1 = std::min(n_pool_chunks, ch0 + B);
         const int64_t Sg = sb + S;
@@ -5061,8 +5105,8 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             int rc = enqueue_fit(fit_enqueued++);
             if (rc) return rc;
         }
-        // ring buffers of super-chunk Sg - 2 (this call's or an earlier one's) are free
-        if (Sg >= 2) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 2) % 3], 0));
+        // ring buffers of super-chunk Sg - 3 (this call's or an earlier one's) are free
+        if (Sg >= 3) HIPCHK(hipStreamWaitEvent(sc, h->gpool[(Sg - 3) % 4], 0));
         if (h->poison) {  // (test aid) the buffers the candidate build is about to fill
             for (int ch = ch0; ch < ch1; ++ch) {
                 const int64_t buf = (c.ring0 + ch) % h->NB;
@@ -5112,11 +5156,16 @@ int run_core(farms_handle *h, Work &w, const int32_t *dx, const int32_t *dy, con
             h->brk.push_back({k0, k1, kBrPoolKernel});
         }
         HIPCHK(hipEventRecord(ev_pk(S), sp));
-        // the previous super-chunk's records, on the chain stream behind this
-        // one's candidate lists: stream P runs nothing but k_pool
-        if (S > 0) { int rc = finish_super(S - 1); if (rc) return rc; }
+        // the records of super-chunk S - 2, on the chain stream behind this
+        // one's candidate lists (stream P runs nothing but the pooling): the
+        // chain's work for S + 1, queued behind that step, waits only for the
+        // pooling of S - 2 and so has the pooling of S - 1 and S to run in.
+        // (Finishing S - 1 here, with a ring of 2B + 1, gave it the pooling of S
+        // alone, and k_true_polar, slowed beside the pooling, held the chain:
+        // C2's pooling stream idled between its launches.)
+        if (S >= lag) { int rc = finish_super(S - lag); if (rc) return rc; }
     }
-    if (n_super > 0) { int rc = finish_super(n_super - 1); if (rc) return rc; }
+    for (int T = std::max(n_super - lag, 0); T < n_super; ++T) { int rc = finish_super(T); if (rc) return rc; }
     while (fit_enqueued < n_fit_chunks) {
         int rc = enqueue_fit(fit_enqueued++);
         if (rc) return rc;
@@ -5268,7 +5317,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         delete h;
         return fail(FARMS_EINVAL, "pool_chunk above 2^24");
     }
-    h->NB = 2 * h->pool_batch + 1;
+    h->NB = 3 * h->pool_batch + 1;
     h->nwords = (h->WH + 63) / 64;
     h->nblk = (int)((h->WH + kGroupCells - 1) / kGroupCells);
     h->cstride = (int64_t)h->nblk * kGroupCells;
@@ -5308,7 +5357,7 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
         hipStreamCreateWithPriority(&h->s_copy, hipStreamNonBlocking, prio_hi) != hipSuccess)  // (device calls: odd fits)
         return bail(fail(FARMS_EHIP, "hipStreamCreate"));
     {
-        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->chain_end, &h->ex_ev, &h->val_ev};
+        std::vector<hipEvent_t *> evs = {&h->gpool[0], &h->gpool[1], &h->gpool[2], &h->gpool[3], &h->chain_end, &h->ex_ev, &h->val_ev};
         for (Work &w : h->ws) {
             evs.push_back(&w.done);
             evs.push_back(&w.ready);
@@ -5776,8 +5825,10 @@ bool is_pinned(const void *p) {
 
 // fn(a, b) over [0, n) split into T slices on host threads (inline when one)
 template <class Fn>
-void host_parallel(int64_t n, int T, Fn &&fn) {
-    const int64_t slice = std::max<int64_t>((n + T - 1) / T, 1 << 16);
+void host_parallel(int64_t n, int T, int64_t align, Fn &&fn) {
+    // slices of at least 2^16 items, multiples of `align`
+    int64_t slice = std::max<int64_t>((n + T - 1) / T, 1 << 16);
+    slice = (slice + align - 1) / align * align;
     std::vector<std::thread> th;
     for (int64_t a = 0; a < n; a += slice) {
         const int64_t b = std::min(n, a + slice);
@@ -5819,7 +5870,7 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         !out->vx || !out->vy || !out->r_local || !out->theta_local || !out->scale)
         return fail(FARMS_EINVAL, "null array");
     HIPCHK(hipSetDevice(h->prm.device));
-    // sub-batches of whole super-chunks, about n / 8 (at least 4 super-chunks);
+    // sub-batches of whole super-chunks, about n / 8 (at least min_sub super-chunks);
     // profiled or counted calls stay one call (their figures are per call)
     const int64_t super = (int64_t)h->pool_chunk * h->pool_batch;
     int64_t sub = n;
@@ -5834,8 +5885,14 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(),
                          what, b);
     };
+    // a sub-batch holds at least FARMS_SUB_MIN (default 8) super-chunks: each
+    // costs a prep on stream F whatever its size (C2, 2M events: 5 sub-batches
+    // of at most 4 super-chunks put the device at 4.2 ms against 2.9 ms for
+    // one call, the host having enqueued everything by 1.7 ms)
+    const char *smv = getenv("FARMS_SUB_MIN");
+    const int64_t min_sub = smv ? std::max(1, atoi(smv)) : 8;
     if (!h->profiling && !h->counting && nsub > 1) {
-        const int64_t per = std::max<int64_t>(4 * super, (n / nsub + super - 1) / super * super);
+        const int64_t per = std::max<int64_t>(min_sub * super, (n / nsub + super - 1) / super * super);
         if (n > 2 * per) sub = per;
     }
     if (sub > kMaxCallEvents) sub = std::max<int64_t>(kMaxCallEvents / super, 1) * super;  // event ids of a sub-batch: 29 bits
@@ -5969,10 +6026,11 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     // although the host enqueued everything within 10 ms; enqueued only when
     // ready they finish within 1 ms of the last pooling launch.
     struct Download { int64_t S, a0; int p0, p1; hipEvent_t done; };
-    auto enqueue_download = [&](const Download &q) -> int {
+    // the copies of the records [g0, g1) of the call (super-chunks S0..S1 - 1,
+    // whose records are final), each super-chunk's completion event after them
+    auto enqueue_download = [&](int64_t S0, int64_t S1, int64_t g0, int64_t g1) -> int {
         hipStream_t sd = h->s_copy;
-        const size_t k = (size_t)(q.p1 - q.p0);
-        const int64_t g0 = q.a0 + q.p0;
+        const size_t k = (size_t)(g1 - g0);
         for (int c = 0; c < 6; ++c)
             HIPCHK(hipMemcpyAsync(dst_col[c] + g0, h->io_rec[c] + g0, 8 * k, hipMemcpyDeviceToHost, sd));
         HIPCHK(hipMemcpyAsync(dst_scale + g0, h->io_scale + g0, 4 * k, hipMemcpyDeviceToHost, sd));
@@ -5980,11 +6038,11 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
         for (int c = 0; c < 4; ++c)
             if (pin_echo[c]) HIPCHK(hipMemcpyAsync(uecho[c] + g0, io_in[c] + g0, 4 * k, hipMemcpyDeviceToHost, sd));
-        HIPCHK(hipEventRecord(h->copy_ev[q.S], sd));
+        for (int64_t S = S0; S < S1; ++S) HIPCHK(hipEventRecord(h->copy_ev[S], sd));
         if (any_host_copy) {
             {
                 std::lock_guard<std::mutex> lk(mu);
-                ready.push_back(Ready{q.S, g0, q.a0 + q.p1});
+                ready.push_back(Ready{S1 - 1, g0, g1});
             }
             cv.notify_one();
         }
@@ -5995,6 +6053,12 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     std::deque<Download> dq;
     bool dclosed = false;
     std::atomic<int> dl_rc{0};
+    // The download thread: waits for the oldest pending super-chunk's records,
+    // then takes with it the following ones already final (their events
+    // complete), so that when the copies lag the compute they go out as one
+    // copy per column over several super-chunks: each copy costs ~10 us of
+    // DMA set-up besides its bytes (C2: 1-MB copies of 25 us, one every 35 us;
+    // the last records landed 1.4 ms after the last pooling launch).
     std::thread dlt([&]() {
         if (hipSetDevice(h->prm.device) != hipSuccess) dl_rc = FARMS_EHIP;
         for (;;) {
@@ -6008,7 +6072,17 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             }
             if (dl_rc) continue;  // a failed download: drain the queue, the call reports it
             if (hipEventSynchronize(q.done) != hipSuccess) { dl_rc = FARMS_EHIP; continue; }
-            if (int r = enqueue_download(q)) dl_rc = r;
+            int64_t S1 = q.S + 1, g1 = q.a0 + q.p1;
+            for (;;) {  // the next ones, while contiguous and final
+                std::lock_guard<std::mutex> lk(dmu);
+                if (dq.empty()) break;
+                const Download &r = dq.front();
+                if (r.S != S1 || r.a0 + r.p0 != g1 || hipEventQuery(r.done) != hipSuccess) break;
+                S1 = r.S + 1;
+                g1 = r.a0 + r.p1;
+                dq.pop_front();
+            }
+            if (int r = enqueue_download(q.S, S1, q.a0 + q.p0, g1)) dl_rc = r;
         }
     });
     auto close_downloads = [&]() {
@@ -6024,20 +6098,35 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
     const bool async = !h->profiling && !h->counting;
     // range check (vFlow.cpp:264 indexes the surfaces unchecked), staging and
     // upload of sub-batch b into the call's device copies (nothing to wait for)
+    // and the sub-batch's candidate plan from the stamps (its pooling chunks
+    // start at the sub-batch's start: bounds are whole super-chunks)
+    std::vector<int> hint(nbat, -1);
     auto upload = [&](int b) -> int {
         const int64_t a0 = bnd[b], m = bnd[b + 1] - a0;
+        const int C2 = h->pool_chunk;
+        const int nch = (int)ceil_div(m, (int64_t)C2);
+        std::vector<uint32_t> tmin(nch, 0xFFFFFFFFu), tmax(nch, 0u);
         std::atomic<int> oor{0};
-        host_parallel(m, T, [&](int64_t i0, int64_t i1) {
+        host_parallel(m, T, C2, [&](int64_t i0, int64_t i1) {
             const int64_t e0 = a0 + i0, k = i1 - i0;
             const int xlo = h->X0, xhi = h->X0 + h->WR, H = h->H;
             int o = 0;
             for (int64_t e = e0; e < e0 + k; ++e) o |= (x[e] < xlo) | (x[e] >= xhi) | (y[e] < 0) | (y[e] >= H);
             if (o) oor = 1;
+            for (int64_t c0 = i0; c0 < i1; c0 += C2) {  // (slices are whole chunks)
+                const uint32_t *tc = t + a0 + c0;
+                const int64_t kc = std::min<int64_t>(C2, i1 - c0);
+                uint32_t lo = 0xFFFFFFFFu, hi = 0;
+                for (int64_t i = 0; i < kc; ++i) { lo = std::min(lo, tc[i]); hi = std::max(hi, tc[i]); }
+                tmin[c0 / C2] = lo;
+                tmax[c0 / C2] = hi;
+            }
             for (int c = 0; c < 4; ++c)
                 if (!pin_in[c]) std::memcpy(stg_in[c] + e0, static_cast<const int32_t *>(uin[c]) + e0, 4 * k);
         });
         tr("staged", b);
         if (oor) return fail(FARMS_EINVAL, "event outside the width x height sensor");
+        hint[b] = host_plan_reach(tmin, tmax) <= kCandMaxBack ? 1 : 0;
         hipStream_t su = h->s_copy;
         int32_t *const io_in[4] = {h->io_x, h->io_y, h->io_t, h->io_p};
         for (int c = 0; c < 4; ++c)
@@ -6054,14 +6143,62 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
         d.scale = h->io_scale + a0;
         return d;
     };
-    int uploaded = 0;
+    // The staging thread: range check, chunk stamp ranges (the sub-batch's
+    // candidate plan) and upload of each sub-batch, at most `ahead` sub-batches
+    // before the compute the main thread enqueues, so that the host's two
+    // chores overlap (C2: ~0.3 ms of staging and ~0.4 ms of enqueue per
+    // sub-batch, one after the other, were the host path's pace).  The upload
+    // of b + 1 goes out before b's compute is enqueued (and before b's
+    // downloads, which share the copy stream).  (Pinned inputs uploaded all up
+    // front: 1.5 ms slower at C3, the burst of uploads slows the first
+    // sub-batches' kernels more.)  FARMS_UPLOAD_AHEAD=0: each sub-batch staged
+    // only once the main thread reaches it (A/B aid).
+    const char *uav = getenv("FARMS_UPLOAD_AHEAD");
+    const int ahead = (uav && uav[0] == '0') ? 0 : 1;
+    std::mutex smu;
+    std::condition_variable scv;
+    int allowed = 0, ok_count = 0, fail_at = -1, st_rc = FARMS_OK;
+    bool st_stop = false;
+    std::string st_err;
+    std::thread stager([&]() {
+        int r = hipSetDevice(h->prm.device) == hipSuccess ? FARMS_OK : fail(FARMS_EHIP, "farms_process: staging thread");
+        for (int b = 0; b < nbat; ++b) {
+            {
+                std::unique_lock<std::mutex> lk(smu);
+                scv.wait(lk, [&] { return b < allowed || st_stop; });
+                if (st_stop) return;
+            }
+            if (r == FARMS_OK) r = upload(b);
+            {
+                std::lock_guard<std::mutex> lk(smu);
+                if (r) { fail_at = b; st_rc = r; st_err = g_err; }
+                else ok_count = b + 1;
+            }
+            scv.notify_all();
+            if (r) return;
+        }
+    });
+    auto stop_stager = [&]() {
+        {
+            std::lock_guard<std::mutex> lk(smu);
+            st_stop = true;
+        }
+        scv.notify_all();
+        stager.join();
+    };
     for (int b = 0; b < nbat && !rc; ++b) {
         const int64_t a0 = bnd[b], m = bnd[b + 1] - a0;
         Work &w = h->ws[b & 1];
-        // (pinned inputs uploaded all up front: 1.5 ms slower at C3, the burst of
-        // uploads slows the first sub-batches' kernels more)
-        while (!rc && uploaded < b + 1) rc = upload(uploaded++);
-        if (rc) break;
+        {
+            std::unique_lock<std::mutex> lk(smu);
+            allowed = std::max(allowed, std::min(b + 1 + ahead, nbat));
+            scv.notify_all();
+            scv.wait(lk, [&] { return ok_count > b || fail_at >= 0; });
+            if (ok_count <= b) {  // this sub-batch's staging failed (out-of-range event, copy)
+                rc = fail(st_rc, st_err);
+                break;
+            }
+        }
         int32_t *const dev_in[4] = {h->io_x + a0, h->io_y + a0, h->io_t + a0, h->io_p + a0};
         if (hipStreamWaitEvent(h->stream, h->up_ev[b], 0) != hipSuccess) {
             rc = fail(FARMS_EHIP, "farms_process: upload wait");
@@ -6083,10 +6220,11 @@ extern "C" int farms_process(farms_handle *h, const int32_t *x, const int32_t *y
             return FARMS_OK;
         };
         rc = run_core(h, w, dev_in[0], dev_in[1], reinterpret_cast<const uint32_t *>(dev_in[2]), dev_in[3], m, &d,
-                      &hook, 0, async, /*validated=*/true);
+                      &hook, 0, async, /*validated=*/true, hint[b]);
         if (rc) break;
         tr("enqueued", b);
     }
+    stop_stager();
     if (trace) {  // when the device finished each stream's work
         (void)hipStreamSynchronize(h->stream); tr("F done", nbat);
         (void)hipStreamSynchronize(h->s_pool); tr("P done", nbat);

@@ -340,6 +340,36 @@ def test_full_size_stream_properties():
     assert int((outs[0]["r_local"] > 0).sum()) > n // 4  # most of the stream is pooled
 
 
+def test_host_path_plan_on_a_stream_that_jumps_back(monkeypatch):
+    """The host-array path decides each sub-batch's candidate build (k_cand or
+    k_chain) from its own copy of the stamps (host_plan_reach) instead of
+    waiting for the device's plan.  A stream whose second half comes first --
+    its stamps jump back by about half the span at the seam, so the chunks past
+    the seam reach back to the first chunk (k_chain) while the others stay
+    time-ordered (k_cand) -- gives bitwise the device path's records, with
+    FARMS_PLAN_CHECK=1 comparing the two plans of every sub-batch."""
+    import torch
+
+    monkeypatch.setenv("FARMS_PLAN_CHECK", "1")
+    ev = farms.synth_config(3, 2_000_000)
+    x, y, t, p = ev.relative()
+    h = len(x) // 2 + 12_345  # the seam inside a sub-batch, not on a chunk boundary
+    x, y, t, p = (np.ascontiguousarray(np.concatenate([a[h:], a[:h]])) for a in (x, y, t, p))
+    n = len(x)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(a).to(dev) for a in (x, y, t.view(np.int32), p)]
+    o = {c: torch.empty(n, dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
+         for c in farms.COLUMNS[4:]}
+    with farms.FlowManager(720, 1280, 5, 5, pool_chunk=1024, pool_batch=8) as fm:
+        fm.process_device(*d, o)
+        fm.reset()
+        g = fm.process(x, y, t, p)
+    dd = {c: v for c, v in zip(farms.COLUMNS[:4], (x, y, t.astype(np.int32), p))}
+    dd.update({c: o[c].cpu().numpy() for c in farms.COLUMNS[4:]})
+    assert bitwise_equal(g, dd)
+    assert int((dd["r_local"] > 0).sum()) > n // 4
+
+
 @pytest.mark.parametrize("threads,pool_chunk,pin", [("1", 1024, "none"), ("3", 2048, "all"), ("8", 0, "mixed"),
                                                     ("8", 1024, "all")])
 def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
@@ -352,6 +382,7 @@ def test_host_path_equals_device_path(threads, pool_chunk, pin, monkeypatch):
     import torch
 
     monkeypatch.setenv("FARMS_HOST_THREADS", threads)
+    monkeypatch.setenv("FARMS_PLAN_CHECK", "1")  # each sub-batch's host-side plan against the device's
     ev = farms.synth_config(3, 3_000_000)
     x, y, t, p = ev.relative()
     n = len(x)

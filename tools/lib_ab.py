@@ -34,7 +34,10 @@ def child(cfg, steps):
     d = [torch.from_numpy(a).to(dev) for a in (x, y, t.view(np.int32), p)]
     o = {c: torch.empty(len(x), dtype=torch.int32 if c == "scale" else torch.float64, device=dev)
          for c in farms.COLUMNS[4:]}
-    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=50)
+    # (FARMS_AB_POOL_BATCH / FARMS_AB_POOL_CHUNK: handle parameters for a sweep)
+    kw = {k: int(os.environ[e]) for k, e in (("pool_batch", "FARMS_AB_POOL_BATCH"), ("pool_chunk", "FARMS_AB_POOL_CHUNK"))
+          if os.environ.get(e)}
+    fm = farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=50, **kw)
     ts = []
     for i in range(steps + 1):
         fm.reset()
@@ -45,7 +48,7 @@ def child(cfg, steps):
         if i:
             ts.append((time.perf_counter() - t0) * 1e3)
     h = int(torch.sum(o["scale"].to(torch.int64) * torch.arange(len(x), device=dev) % 1000003).item())
-    print(json.dumps({"lib": os.environ.get("FARMS_HIP_LIB", "default"), "config": cfg, "events": len(x),
+    print(json.dumps({"lib": os.environ.get("FARMS_HIP_LIB", "default"), "config": cfg, "events": len(x), **kw,
                       "ms_best": round(min(ts), 2), "ms_mean": round(sum(ts) / len(ts), 2), "scale_hash": h}),
           flush=True)
 

@@ -167,6 +167,14 @@ def parity_vs_cpu(ref, out, k):
             "scale_mismatch": rep["scale_mismatch"], "ok": rep["ok"]}
 
 
+def profile_split(split: str, world: int) -> str:
+    """The split whose committed PMC summaries a line's roofline reads: one GPU
+    runs the whole-sensor call whatever the config's split for N > 1 (round 6:
+    C4/C5 default to strips, and their N=1 lines read none of the strip
+    summaries)."""
+    return split if world > 1 else "none"
+
+
 def committed_profile(kind: str, cfg: int, split: str, kernel: str):
     """Per-kernel PMC figures of the newest committed rocprofv3 summary of the
     same per-GPU workload: profiles/rNN_<kind>_c<cfg>.json (tools/gpu_traffic.sh /
@@ -475,7 +483,7 @@ def main():
     fm.set_profiling(True)
     st.step()
     cs = fm.stats()
-    rl = rooflines(cfg, args.split, ts, cs, fm.kernel_info())
+    rl = rooflines(cfg, profile_split(args.split, world), ts, cs, fm.kernel_info())
     dom = rl["dominant"]
     mine = {"rank": rank, "ms_step_rank": round(elapsed_rank / args.steps * 1e3, 3),
             "stored_events": n, "owned_events": n_owned,

@@ -133,3 +133,17 @@ def test_rooflines_use_busy_wall_time_for_overlapping_launches():
     assert f["ms_busy_per_step"] == 56.6 and f["ms_bracket_sum_per_step"] == 93.7
     assert rl["dominant"] == "k_fit"
     assert f["launches_per_step"] * f["avg_launch_us"] / 1e3 <= 61.4
+
+
+def test_one_gpu_lines_read_the_whole_sensor_pmc_summaries():
+    """Configs 4 and 5 default to x-strips for N > 1; their one-GPU lines still
+    run the whole-sensor call and take its committed PMC traffic (the round-6
+    lines first looked for strip summaries and reported frac null)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.profile_split("strips", 1) == "none" and bench.profile_split("strips", 4) == "strips"
+    for cfg in (4, 5):
+        tr = bench.committed_profile("traffic", cfg, bench.profile_split(bench.default_split(cfg), 1),
+                                     "k_fit_quad<3>")
+        assert tr and tr["traffic_bytes_per_launch"] > 0 and "_strips" not in tr["source"]

@@ -2318,36 +2318,53 @@ __global__ void k_cand_list(Ctx c, int4 *list) {
 // k_fit_desc, k_band_starts and k_chunk_minmax for pooling chunks of 2,048,
 // 4,096 and 8,192 events (C3 77.6-77.8 -> 77.2 ms per step,
 // profiles/r04_ab_chunk_order.log).
+// The events' fields are read and the work order / descriptors written in
+// striped order (lane-consecutive ranks: coalesced); the blocked arrangement
+// the stable sort takes is made through LDS on both sides (round 6: C3 67.1 ->
+// 66.1 ms, profiles/r06_ab_chunk_order_striped_c3.log; the blocked reads and
+// writes touched a 32-B-strided line per lane).
 template <int THREADS, int ITEMS>
 __global__ __launch_bounds__(THREADS) void k_chunk_order(Ctx c, int tile_bits, int32_t *Q, int32_t *bstart,
                                                          uint32_t *tmin, uint32_t *tmax) {
     using BRS = hipcub::BlockRadixSort<uint32_t, THREADS, ITEMS, int>;
-    __shared__ typename BRS::TempStorage s_sort;
-    __shared__ uint32_t s_last[THREADS];
+    constexpr int N = THREADS * ITEMS;
+    __shared__ union {
+        typename BRS::TempStorage sort;
+        uint32_t key[N];
+        uint2 kv[N];
+    } s_u;
     __shared__ uint32_t s_lo[THREADS / 64], s_hi[THREADS / 64];
     const int ch = (int)blockIdx.x, tid = (int)threadIdx.x;
     const int cs = ch * c.C2, cnt = min(c.C2, c.n - cs);
     const uint32_t pad = 1u << tile_bits;
-    uint32_t key[ITEMS];
-    int val[ITEMS];
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int r = tid * ITEMS + i;
-        val[i] = r;
-        key[i] = pad;
+    for (int i = 0; i < ITEMS; ++i) {  // striped: rank i * THREADS + tid
+        const int r = i * THREADS + tid;
+        uint32_t k = pad;
         if (r < cnt) {
             const int e = cs + r;
             const int x = c.x[e], y = c.y[e];
             const uint32_t t = c.t[e];
-            key[i] = (uint32_t)((x - c.X0) >> c.tshift) * (uint32_t)c.tilesH + (uint32_t)(y >> c.tshift);
+            k = (uint32_t)((x - c.X0) >> c.tshift) * (uint32_t)c.tilesH + (uint32_t)(y >> c.tshift);
             lo = t < lo ? t : lo;
             hi = t > hi ? t : hi;
         }
+        s_u.key[r] = k;
     }
-    BRS(s_sort).Sort(key, val, 0, tile_bits + 1);
-    // blocked output: thread tid holds ranks tid * ITEMS + i, ascending
-    s_last[tid] = key[ITEMS - 1];
+    __syncthreads();
+    uint32_t key[ITEMS];
+    int val[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {  // blocked: rank tid * ITEMS + i (the stable sort's input order)
+        key[i] = s_u.key[tid * ITEMS + i];
+        val[i] = tid * ITEMS + i;
+    }
+    __syncthreads();
+    BRS(s_u.sort).Sort(key, val, 0, tile_bits + 1);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) s_u.kv[tid * ITEMS + i] = make_uint2(key[i], (uint32_t)val[i]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
@@ -2358,22 +2375,22 @@ __global__ __launch_bounds__(THREADS) void k_chunk_order(Ctx c, int tile_bits, i
     const int tpb = c.bandc >> c.tshift;  // tile columns per band
     auto band = [&](uint32_t k) { return k >= pad ? c.nbands : (int)(k / (uint32_t)c.tilesH) / tpb; };
     int32_t *bs = bstart + (int64_t)ch * (c.nbands + 1);
-    int prev = tid > 0 ? band(s_last[tid - 1]) : -1;
 #pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int r = tid * ITEMS + i;
-        const int b = band(key[i]);
+    for (int i = 0; i < ITEMS; ++i) {  // striped again: coalesced Q / descriptor writes
+        const int r = i * THREADS + tid;
+        const uint2 kv = s_u.kv[r];
+        const int b = band(kv.x);
+        const int prev = r > 0 ? band(s_u.kv[r - 1].x) : -1;
         // the first rank of each band (padding ranks have band nbands: its start is cnt)
         for (int q = prev + 1; q <= b; ++q) bs[q] = cs + min(r, cnt);
-        prev = b;
+        if (r == N - 1)  // bands past the last key (no padding when the chunk is full)
+            for (int q = b + 1; q <= c.nbands; ++q) bs[q] = cs + cnt;
         if (r < cnt) {
-            const int e = cs + val[i];
+            const int e = cs + (int)kv.y;
             Q[cs + r] = e;
             c.fdesc[cs + r] = make_int4(e, c.x[e], c.y[e], (int)c.t[e]);
         }
     }
-    if (tid == THREADS - 1)  // bands past the last key (no padding when the chunk is full)
-        for (int q = prev + 1; q <= c.nbands; ++q) bs[q] = cs + cnt;
     if (tid == 0) {
         uint32_t a = s_lo[0], b = s_hi[0];
         for (int u = 1; u < THREADS / 64; ++u) { a = min(a, s_lo[u]); b = max(b, s_hi[u]); }

@@ -4341,6 +4341,22 @@ int sync_all(farms_handle *h) {
     return FARMS_OK;
 }
 
+// The pixel sort of a call's events (stable, by pixel id over end_bit bits):
+// rocPRIM's onesweep with 10 bits per pass, two passes for a 1280x720 sensor's
+// 20-bit ids where hipCUB's gfx950 default (8 bits) takes three (C3 66.4 ->
+// 66.1, C2 2.90 -> 2.85 ms, same bits; 11 bits: 66.8,
+// profiles/r06_ab_sort_bits.log).  (The 1,024-thread blocks rank with
+// per-wave counters, `match`: the default per-thread ones need 2 MB of LDS at
+// 10 bits.)
+hipError_t pixel_sort(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const int32_t *vin, int32_t *vout,
+                      int n, int end_bit, hipStream_t s) {
+    using Cfg = rocprim::radix_sort_config<
+        rocprim::default_config, rocprim::default_config,
+        rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 10,
+                                            rocprim::block_radix_rank_algorithm::match>>;
+    return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, s);
+}
+
 int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
     if (n <= w.cap) return FARMS_OK;
     int rc = sync_all(h);  // the set may still be read by an earlier call
@@ -4361,8 +4377,7 @@ int ensure_capacity(farms_handle *h, Work &w, int64_t n) {
         return rc;
     }
     size_t bytes = 0, bytes2 = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, w.pix, w.skey, w.iota, w.P, (int)cap, 0,
-                                              end_bit_for(h->WH), h->stream));
+    HIPCHK(pixel_sort(nullptr, bytes, w.pix, w.skey, w.iota, w.P, (int)cap, end_bit_for(h->WH), h->stream));
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, w.wkey, w.wkey_sorted, w.iota, w.Q, (int)cap, 0,
                                               32, h->stream));
     bytes = std::max(bytes, bytes2);
@@ -4821,8 +4836,7 @@ int enqueue_prep(farms_handle *h, Work &w, const Ctx &c, int n, bool validated, 
     hipLaunchKernelGGL(k_prep, dim3(ceil_div(n, 256)), dim3(256), 0, s, c, w.pix, w.iota, w.wkey, h->err + 1,
                        h->pool_chunk, h->tile_bits, h->tile_shift);
     size_t bytes = w.cub_bytes;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(w.cub_tmp, bytes, w.pix, w.skey, w.iota, w.P, n, 0,
-                                              end_bit_for(h->WH), s));
+    HIPCHK(pixel_sort(w.cub_tmp, bytes, w.pix, w.skey, w.iota, w.P, n, end_bit_for(h->WH), s));
     HIPCHK(hipMemsetAsync(w.pend, 0xFF, sizeof(int32_t) * h->WH, s));  // cells without events in this call
     // serial mode: k_link reads the flow snapshots' stamps, final once the
     // previous call's chain is done

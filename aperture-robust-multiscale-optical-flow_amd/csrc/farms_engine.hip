@@ -5338,8 +5338,19 @@ extern "C" int farms_create(const farms_params *prm, farms_handle **out) {
        // linear size of the stored region (nearest power of two; 320x320: 2048,
        // measured best; an x-strip of 4 or 8 on 1280x720: 4096, so that its
        // chunks span a time closer to a whole-sensor chunk's)
+        const int base = h->pool_chunk;
         const double target = h->pool_chunk * std::sqrt((double)h->WR * h->H / (1280.0 * 720.0));
         while (h->pool_chunk > 1024 && h->pool_chunk > target * std::sqrt(2.0)) h->pool_chunk /= 2;
+        // regions that keep the base size (the whole 1280x720 sensor, a half
+        // strip of it): 4,096-event chunks, whose candidate lists hold fewer
+        // cells too old for most of the chunk's events, in longer super-chunks
+        // at fs 5 (round 6 sweep, profiles/r06_ab_pool_chunk_sweep.log: C3
+        // 66.0 -> 64.7 ms at 4096 x 192, 65.2 at x 128, 66.1 at x 64; C4 51.8
+        // -> 48.2 at 4096 x 64, 49.5-50.0 at 8192 x 64/96/128 and 4096 x 128)
+        if (h->pool_chunk == base && prm->pool_chunk <= 0) {  // (an explicit chunk keeps its batch default)
+            h->pool_chunk = 4096;
+            h->pool_batch = h->fr == 3 ? kDefaultPoolBatch : 3 * kDefaultPoolBatch;
+        }
     }
     if (prm->fit_chunk > 0) h->fit_chunk = prm->fit_chunk;
     if (prm->pool_chunk > 0) h->pool_chunk = prm->pool_chunk;

@@ -44,7 +44,10 @@ def main():
     own = [farms.pinned(v) for v in (x, y, t, p)]
     rec = farms.Records(len(x), pinned=True)
     res = {"config": cfg, "events": len(x), "env": {k: v for k, v in os.environ.items() if k.startswith("FARMS_")}}
-    with farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=50) as fm:
+    # (FARMS_AB_POOL_BATCH / FARMS_AB_POOL_CHUNK: handle parameters, as tools/lib_ab.py)
+    kw = {k: int(os.environ[e]) for k, e in (("pool_batch", "FARMS_AB_POOL_BATCH"), ("pool_chunk", "FARMS_AB_POOL_CHUNK"))
+          if os.environ.get(e)}
+    with farms.FlowManager(H, W, fs, 5, window_jump=jump, max_window=50, **kw) as fm:
         def timed(fn):
             ts = []
             for i in range(a.steps + 1):

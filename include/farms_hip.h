@@ -45,8 +45,9 @@ typedef struct {
     int32_t window_jump;  /* pooling scale step, reference 5 */
     int32_t max_window;   /* largest pooling radius, reference 50 */
     int32_t device;       /* HIP device ordinal */
-    int32_t fit_chunk;    /* events per local-fit chunk, 0 = default (65536; 131072 at filtersize 7) */
-    int32_t pool_chunk;   /* events per pooling chunk, 0 = default (8192, 16384 at filtersize 7; less on sensors under 1280x720) */
+    int32_t fit_chunk;    /* events per local-fit chunk, 0 = default (65536) */
+    int32_t pool_chunk;   /* events per pooling chunk, 0 = default (4096 where the stored region is at least about half of
+                             1280x720; scaled down from 8192 (16384 at filtersize 7) on smaller regions) */
     /* spatial strips (multi-GPU): the handle stores columns [region_x0,
      * region_x0 + region_width) of the width x height sensor and pools only the
      * events of columns [own_x0, own_x1); events of the other stored columns are
@@ -57,7 +58,8 @@ typedef struct {
      * sensor), owned records are bitwise those of a whole-sensor run. */
     int32_t region_x0, region_width;
     int32_t own_x0, own_x1;
-    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64; 32 at filtersize 7) */
+    int32_t pool_batch;   /* pooling chunks per pooling launch, 0 = default (64; 32 at filtersize 7 on scaled-down
+                             regions; with the 4096-event default chunk: 192, 64 at filtersize 7) */
     /* 1: the per-event semantics of vFlowManager::run (vFlow.cpp:465-826, the
      * CLI's --SERIAL 1, its default): lastEventTime is written after pooling
      * (:790), so an event's own cell is pooled with the stamp of the previous
